@@ -1,0 +1,63 @@
+/*
+ * leopard_amd.h -- MI355X-specific extensions of the Leopard C ABI.
+ *
+ * None of these is needed for drop-in use (include/leopard.h is the contract);
+ * they let a GPU-resident caller avoid the synchronous host-memory semantics of
+ * the reference (leopard.h:180-234 return only when results are written).
+ */
+#ifndef LEOPARD_AMD_EXT_H
+#define LEOPARD_AMD_EXT_H
+
+#include "leopard.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* HIP stream used by the calling thread's leo_encode/leo_decode on device
+ * memory (a hipStream_t passed as void*; NULL = the legacy default stream).
+ * Per thread. */
+LEO_EXPORT void leo_amd_set_stream(void* hip_stream);
+
+/* 1: device-resident calls return after enqueueing work on the stream (the
+ * caller orders later reads on that stream).  0 (default): every call
+ * synchronises, like the reference.  Host-memory calls are always synchronous.
+ * Per thread. */
+LEO_EXPORT void leo_amd_set_async(int async_enable);
+
+/* Device ordinal the calling thread's calls run on (default: the current HIP
+ * device at call time).  -1 restores the default.  Per thread. */
+LEO_EXPORT void leo_amd_set_device(int device);
+
+/* Encode/decode a column range of every piece: identical to leo_encode /
+ * leo_decode over bytes [byte_offset, byte_offset + slice_bytes) of each
+ * piece (both multiples of 64).  This is how independent GPUs shard one object
+ * by 64-byte column blocks without any collective (each GPU owns a slice). */
+LEO_EXPORT LeopardResult leo_amd_encode_slice(
+    uint64_t buffer_bytes, uint64_t byte_offset, uint64_t slice_bytes,
+    unsigned original_count, unsigned recovery_count, unsigned work_count,
+    const void* const* const original_data, void** work_data);
+
+LEO_EXPORT LeopardResult leo_amd_decode_slice(
+    uint64_t buffer_bytes, uint64_t byte_offset, uint64_t slice_bytes,
+    unsigned original_count, unsigned recovery_count, unsigned work_count,
+    const void* const* const original_data, const void* const* const recovery_data,
+    void** work_data);
+
+/* Number of HIP devices usable by the library (0 when none / not gfx950). */
+LEO_EXPORT int leo_amd_device_count(void);
+
+/* Host-side tables, for conformance tests (no GPU needed).  field: 8 or 16.
+ * which: 0 = log (Cantor basis), 1 = exp, 2 = FFT skew (as logs), 3 = LogWalsh.
+ * Copies up to `capacity` uint16 entries into out; returns the table length,
+ * or a negative LeopardResult. */
+LEO_EXPORT int leo_amd_table(int field, int which, uint16_t* out, unsigned capacity);
+
+/* Human-readable description of the last error on the calling thread. */
+LEO_EXPORT const char* leo_amd_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LEOPARD_AMD_EXT_H */

@@ -1,0 +1,71 @@
+// gf_tables.h -- host-side construction of the GF(2^8)/GF(2^16) tables that the
+// device kernels consume.  Built once in leo_init() (reference: ff8/ff16
+// Initialize(), LeopardFF8.cpp:1922-1935, LeopardFF16.cpp:1781-1794).
+#pragma once
+
+#include <cstdint>
+#include <vector>
+
+namespace lamd {
+
+// One binary extension field in Leopard's Cantor-basis representation.
+//   log_of[x]   : discrete log of the element whose Cantor coordinates are x
+//                 (log_of[0] == modulus, i.e. "zero"),     LeopardFF8.cpp:158-194
+//   exp_of[l]   : inverse map, exp_of[modulus] == exp_of[0]
+//   skew[i]     : FFT skew factors as logs (modulus == the zero element),
+//                 eq. (28) of Lin-Chung-Han,                LeopardFF8.cpp:496-531
+//   log_walsh[i]: FWHT of log_of (log_of[0] := 0),          LeopardFF8.cpp:533-537
+class GaloisField {
+public:
+    GaloisField(unsigned bits, unsigned polynomial, const uint16_t* cantor_basis);
+
+    unsigned bits() const { return bits_; }
+    unsigned order() const { return order_; }
+    unsigned modulus() const { return modulus_; }
+
+    // Partially reduced mod 2^bits - 1 (the modulus itself stands for 0).
+    unsigned add_mod(unsigned a, unsigned b) const {
+        unsigned s = a + b;
+        return (s + (s >> bits_)) & modulus_;
+    }
+    unsigned sub_mod(unsigned a, unsigned b) const {
+        unsigned d = a - b;
+        return (d + (d >> bits_)) & modulus_;
+    }
+    // x * exp(log_m): the only multiply Leopard ever performs (LeopardFF8.cpp:141-154).
+    unsigned mul_log(unsigned x, unsigned log_m) const {
+        return x == 0 ? 0u : exp_of[add_mod(log_of[x], log_m)];
+    }
+    // In-place Walsh-Hadamard transform mod 2^bits - 1 over `n` entries.
+    void walsh(uint16_t* v, unsigned n) const;
+
+    std::vector<uint16_t> log_of, exp_of, skew, log_walsh;
+
+private:
+    void build_logs(unsigned polynomial, const uint16_t* basis);
+    void build_skews();
+
+    unsigned bits_, order_, modulus_;
+};
+
+const GaloisField& field8();
+const GaloisField& field16();
+
+// Byte-permute multiply tables consumed by v_perm_b32 (see rs_device.h).
+//
+// FF8, 8 dwords per log value L (entries are products x * exp(L)):
+//   [0..1] 8 entries for input bits 0-2     [2..3] bits 3-5
+//   [4]    4 entries for input bits 6-7     [5..7] zero padding
+// FF16, 24 dwords per log value L (element = lo | hi << 8; every input chunk
+// gives a 16-bit product, split into a low-byte table and a high-byte table):
+//   chunk lo[0-2]: [0..1] lo-byte, [2..3] hi-byte     chunk lo[3-5]: [4..7]
+//   chunk hi[0-2]: [8..11]                             chunk hi[3-5]: [12..15]
+//   chunk lo[6-7]: [16] lo-byte, [17] hi-byte          chunk hi[6-7]: [18], [19]
+//   [20..23] zero padding
+// Both arrays carry one extra all-zero table at index order (multiply by 0).
+constexpr unsigned kTab8Dwords = 8;
+constexpr unsigned kTab16Dwords = 24;
+void build_perm_tables8(const GaloisField& f, std::vector<uint32_t>& out);
+void build_perm_tables16(const GaloisField& f, std::vector<uint32_t>& out);
+
+}  // namespace lamd

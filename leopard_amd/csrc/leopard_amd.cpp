@@ -1,0 +1,820 @@
+// leopard_amd.cpp -- the drop-in C ABI (include/leopard.h) over the gfx950 kernels.
+//
+// Replaces the reference's leopard.cpp dispatch (leopard.cpp:49-344): same
+// validation order, result codes, work counts and edge paths (K == 1, R == 1,
+// no loss), with the codec bodies (ReedSolomonEncode/Decode) running as HIP
+// kernels instead of ff8::/ff16:: SIMD loops.  There is no CPU fallback: with no
+// usable GPU leo_init() returns Leopard_Platform and every call fails loudly.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/leopard.h"
+#include "../../include/leopard_amd.h"
+#include "gf_tables.h"
+#include "rs_args.h"
+
+namespace lamd {
+namespace {
+
+// ------------------------------------------------------------ thread state --
+
+struct ThreadState {
+    hipStream_t stream = nullptr;
+    bool async = false;
+    int device = -1;
+    std::string last_error;
+};
+thread_local ThreadState tls;
+
+void set_error(const char* what, hipError_t e) {
+    char buf[256];
+    std::snprintf(buf, sizeof(buf), "%s: %s", what, hipGetErrorString(e));
+    tls.last_error = buf;
+}
+
+#define HIP_OK(expr, what)                         \
+    do {                                           \
+        hipError_t e_ = (expr);                    \
+        if (e_ != hipSuccess) {                    \
+            set_error(what, e_);                   \
+            return Leopard_Platform;               \
+        }                                          \
+    } while (0)
+
+// ----------------------------------------------------- per-device resources --
+
+struct DeviceTables {
+    uint32_t* tab8 = nullptr;   // (256 + 1) x 8 dwords
+    uint32_t* tab16 = nullptr;  // (65536 + 1) x 24 dwords
+    uint32_t* skew8 = nullptr;  // 255 (+1 pad) entries
+    uint32_t* skew16 = nullptr;
+    uint32_t* walsh8 = nullptr;
+    uint32_t* walsh16 = nullptr;
+    uint8_t* zeros = nullptr;   // zero page
+    bool ready = false;
+};
+
+std::mutex g_mu;
+bool g_initialized = false;
+int g_device_count = 0;
+std::vector<DeviceTables> g_dev;
+std::vector<uint32_t> g_h_tab8, g_h_tab16, g_h_skew8, g_h_skew16, g_h_walsh8, g_h_walsh16;
+
+template <class T>
+hipError_t upload(T** dst, const std::vector<T>& src) {
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(dst), src.size() * sizeof(T));
+    if (e != hipSuccess) return e;
+    return hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice);
+}
+
+LeopardResult ensure_device(int dev, DeviceTables** out) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (dev < 0 || dev >= int(g_dev.size())) {
+        tls.last_error = "device ordinal out of range";
+        return Leopard_Platform;
+    }
+    DeviceTables& d = g_dev[dev];
+    if (!d.ready) {
+        HIP_OK(upload(&d.tab8, g_h_tab8), "upload FF8 tables");
+        HIP_OK(upload(&d.tab16, g_h_tab16), "upload FF16 tables");
+        HIP_OK(upload(&d.skew8, g_h_skew8), "upload FF8 skew");
+        HIP_OK(upload(&d.skew16, g_h_skew16), "upload FF16 skew");
+        HIP_OK(upload(&d.walsh8, g_h_walsh8), "upload FF8 LogWalsh");
+        HIP_OK(upload(&d.walsh16, g_h_walsh16), "upload FF16 LogWalsh");
+        HIP_OK(hipMalloc(reinterpret_cast<void**>(&d.zeros), 4096), "zero page");
+        HIP_OK(hipMemset(d.zeros, 0, 4096), "zero page");
+        d.ready = true;
+    }
+    *out = &d;
+    return Leopard_Success;
+}
+
+// Per-thread, per-device scratch: device arena (grow-only) plus a pinned host
+// staging area for pointer tables / bitmaps.
+struct Workspace {
+    int dev = -1;
+    uint8_t* dbuf = nullptr;
+    size_t dsize = 0;
+    uint8_t* hstage = nullptr;
+    size_t hsize = 0;
+    hipEvent_t stage_done = nullptr;
+    bool stage_pending = false;
+
+    ~Workspace() {
+        // Process teardown: the runtime may already be gone; leak rather than crash.
+    }
+    LeopardResult reserve_device(size_t bytes) {
+        if (bytes <= dsize) return Leopard_Success;
+        if (dbuf) {
+            HIP_OK(hipDeviceSynchronize(), "sync before scratch growth");
+            HIP_OK(hipFree(dbuf), "free scratch");
+            dbuf = nullptr;
+        }
+        size_t want = std::max(bytes, dsize * 2);
+        HIP_OK(hipMalloc(reinterpret_cast<void**>(&dbuf), want), "allocate scratch");
+        dsize = want;
+        return Leopard_Success;
+    }
+    // Staging buffer free for writing (previous upload finished).
+    LeopardResult reserve_stage(size_t bytes) {
+        if (stage_pending) {
+            HIP_OK(hipEventSynchronize(stage_done), "wait staging");
+            stage_pending = false;
+        }
+        if (!stage_done) HIP_OK(hipEventCreateWithFlags(&stage_done, hipEventDisableTiming), "event");
+        if (bytes <= hsize) return Leopard_Success;
+        if (hstage) HIP_OK(hipHostFree(hstage), "free staging");
+        hstage = nullptr;
+        size_t want = std::max<size_t>(bytes, std::max<size_t>(hsize * 2, 1 << 16));
+        HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&hstage), want, hipHostMallocDefault), "pinned staging");
+        hsize = want;
+        return Leopard_Success;
+    }
+};
+thread_local std::vector<std::unique_ptr<Workspace>> tws;
+
+Workspace& workspace(int dev) {
+    if (int(tws.size()) <= dev) tws.resize(dev + 1);
+    if (!tws[dev]) {
+        tws[dev] = std::make_unique<Workspace>();
+        tws[dev]->dev = dev;
+    }
+    return *tws[dev];
+}
+
+// ------------------------------------------------------------ call helpers --
+
+unsigned next_pow2(unsigned n) {
+    unsigned p = 1;
+    while (p < n) p <<= 1;
+    return p;
+}
+unsigned log2u(unsigned n) {
+    unsigned t = 0;
+    while ((1u << t) < n) ++t;
+    return t;
+}
+
+enum class MemKind { Device, Host };
+
+// Pointer kind from the first non-null pointer (all pieces of a call must agree).
+MemKind classify(const void* p, int* dev) {
+    hipPointerAttribute_t attr;
+    std::memset(&attr, 0, sizeof(attr));
+    hipError_t e = hipPointerGetAttributes(&attr, p);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return MemKind::Host;
+    }
+    if (attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged) {
+        *dev = attr.device;
+        return MemKind::Device;
+    }
+    return MemKind::Host;
+}
+
+// Builds a PieceMap: a slab (base + i*stride) when the non-null pointers are
+// equally spaced, else a device pointer table written into `tables` (pinned
+// staging, uploaded by the caller).
+struct MapBuilder {
+    std::vector<uint64_t> staged;  // host image of all tables of this call
+    struct Pending {
+        PieceMap* map;
+        size_t index;
+    };
+    std::vector<Pending> pending;
+
+    void build(PieceMap& pm, const void* const* ptrs, unsigned count, uint64_t off) {
+        pm = PieceMap{nullptr, nullptr, 0, off};
+        int i0 = -1, i1 = -1;
+        for (unsigned i = 0; i < count; ++i) {
+            if (!ptrs[i]) continue;
+            if (i0 < 0) i0 = int(i);
+            else { i1 = int(i); break; }
+        }
+        if (i0 < 0) return;  // nothing present; never dereferenced
+        int64_t stride = 0;
+        bool slab = true;
+        const int64_t p0 = int64_t(reinterpret_cast<uintptr_t>(ptrs[i0]));
+        if (i1 >= 0) {
+            const int64_t d = int64_t(reinterpret_cast<uintptr_t>(ptrs[i1])) - p0;
+            if (d % (i1 - i0) != 0) slab = false;
+            else stride = d / (i1 - i0);
+        }
+        for (unsigned i = unsigned(i0); slab && i < count; ++i)
+            if (ptrs[i] && int64_t(reinterpret_cast<uintptr_t>(ptrs[i])) != p0 + (int64_t(i) - i0) * stride) slab = false;
+        if (slab) {
+            pm.base = reinterpret_cast<uint8_t*>(uintptr_t(p0 - int64_t(i0) * stride));
+            pm.stride = uint64_t(stride);
+            return;
+        }
+        const size_t at = staged.size();
+        for (unsigned i = 0; i < count; ++i) staged.push_back(uint64_t(reinterpret_cast<uintptr_t>(ptrs[i])));
+        pending.push_back({&pm, at});
+    }
+    size_t bytes() const { return staged.size() * sizeof(uint64_t); }
+    // Copies the tables into pinned staging and enqueues the H2D copy into dev.
+    LeopardResult flush(Workspace& ws, uint64_t* dev, hipStream_t s) {
+        if (staged.empty()) return Leopard_Success;
+        LeopardResult r = ws.reserve_stage(bytes());
+        if (r != Leopard_Success) return r;
+        std::memcpy(ws.hstage, staged.data(), bytes());
+        HIP_OK(hipMemcpyAsync(dev, ws.hstage, bytes(), hipMemcpyHostToDevice, s), "upload piece tables");
+        HIP_OK(hipEventRecord(ws.stage_done, s), "record staging");
+        ws.stage_pending = true;
+        for (auto& p : pending) p.map->table = dev + p.index;
+        return Leopard_Success;
+    }
+};
+
+// Column range processed per pass sequence of the multi-pass FF16 kernels:
+// keep the intermediates (pieces x slice) around the 256 MiB Infinity Cache.
+uint64_t mall_slice(uint64_t bytes, uint64_t slab_pieces) {
+    const uint64_t budget = 160ull << 20;
+    uint64_t slice = budget / std::max<uint64_t>(slab_pieces, 1);
+    slice = std::max<uint64_t>(slice / 512 * 512, 512);  // whole FF16 tiles (64 units x 8 B)
+    return std::min(slice, bytes);
+}
+
+struct Call {
+    int dev = 0;
+    DeviceTables* t = nullptr;
+    Workspace* ws = nullptr;
+    hipStream_t s = nullptr;
+};
+
+LeopardResult begin_call(int dev, Call& c) {
+    LeopardResult r = ensure_device(dev, &c.t);
+    if (r != Leopard_Success) return r;
+    c.dev = dev;
+    c.ws = &workspace(dev);
+    c.s = tls.stream;
+    return Leopard_Success;
+}
+
+LeopardResult finish(const Call& c, bool force_sync) {
+    HIP_OK(hipGetLastError(), "kernel launch");
+    if (force_sync || !tls.async) HIP_OK(hipStreamSynchronize(c.s), "stream synchronize");
+    return Leopard_Success;
+}
+
+// --------------------------------------------------------------- encode ----
+
+// Device-resident encode of pieces [off, off + bytes) (reference:
+// leo_encode -> ff8|ff16::ReedSolomonEncode, leopard.cpp:162-197).
+LeopardResult encode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, unsigned R, const void* const* orig,
+                            void** work) {
+    const unsigned m = next_pow2(R);
+    const unsigned n = next_pow2(m + K);
+    const bool ff16 = n > 256;
+    const unsigned Tm = log2u(m);
+    const unsigned nchunks = (K + m - 1) / m;
+
+    EncArgs a;
+    std::memset(&a, 0, sizeof(a));
+    MapBuilder mb;
+    mb.build(a.in, orig, K, off);
+    mb.build(a.out, work, R, off);
+    a.skew = ff16 ? c.t->skew16 : c.t->skew8;
+    a.tabs = ff16 ? c.t->tab16 : c.t->tab8;
+    a.zeros = c.t->zeros;
+    a.K = K;
+    a.R = R;
+    a.Tm = Tm;
+    a.nchunks = nchunks;
+    const unsigned unit_bytes = ff16 ? 8 : 4;
+
+    const bool multipass = ff16 && Tm > kLoBits;
+    uint64_t slice = bytes, slab_bytes = 0;
+    if (multipass) {
+        const uint64_t slab_pieces = uint64_t(nchunks) * m + m;
+        slice = mall_slice(bytes, slab_pieces);
+        slab_bytes = slab_pieces * slice;
+    }
+    const size_t table_bytes = (mb.bytes() + 255) / 256 * 256;
+    LeopardResult r = c.ws->reserve_device(table_bytes + slab_bytes);
+    if (r != Leopard_Success) return r;
+    r = mb.flush(*c.ws, reinterpret_cast<uint64_t*>(c.ws->dbuf), c.s);
+    if (r != Leopard_Success) return r;
+
+    if (!multipass) {
+        a.nunits = bytes / unit_bytes;
+        HIP_OK(launch_encode_fused(ff16, Tm, a, c.s), "encode kernel");
+        return Leopard_Success;
+    }
+    uint8_t* U = c.ws->dbuf + table_bytes;
+    uint8_t* V = U + uint64_t(nchunks) * m * slice;
+    for (uint64_t pos = 0; pos < bytes; pos += slice) {
+        const uint64_t len = std::min(slice, bytes - pos);
+        EncArgs b = a;
+        b.in.off = off + pos;
+        b.out.off = off + pos;
+        b.slab_out = PieceMap{nullptr, U, slice, 0};
+        b.nunits = len / unit_bytes;
+        HIP_OK(launch_encode_lo(b, c.s), "encode pass 1");
+        b.slab_in = PieceMap{nullptr, U, slice, 0};
+        b.slab_out = PieceMap{nullptr, V, slice, 0};
+        HIP_OK(launch_encode_hi(b, c.s), "encode pass 2");
+        b.slab_in = PieceMap{nullptr, V, slice, 0};
+        HIP_OK(launch_encode_fin(b, c.s), "encode pass 3");
+    }
+    return Leopard_Success;
+}
+
+// XOR of `count` pieces into out (R == 1 paths).
+LeopardResult xor_device(Call& c, uint64_t bytes, uint64_t off, const void* const* src, unsigned count, void* out) {
+    XorArgs a;
+    std::memset(&a, 0, sizeof(a));
+    MapBuilder mb;
+    mb.build(a.src, src, count, off);
+    void* outs[1] = {out};
+    mb.build(a.out, outs, 1, off);
+    a.count = count;
+    a.ndwords = bytes / 4;
+    LeopardResult r = c.ws->reserve_device((mb.bytes() + 255) / 256 * 256);
+    if (r != Leopard_Success) return r;
+    r = mb.flush(*c.ws, reinterpret_cast<uint64_t*>(c.ws->dbuf), c.s);
+    if (r != Leopard_Success) return r;
+    HIP_OK(launch_xor_reduce(a, c.s), "xor kernel");
+    return Leopard_Success;
+}
+
+// --------------------------------------------------------------- decode ----
+
+LeopardResult decode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, unsigned R, const void* const* orig,
+                            const void* const* rec, void** work) {
+    const unsigned m = next_pow2(R);
+    const unsigned n = next_pow2(m + K);
+    const bool ff16 = n > 256;
+    const unsigned Tn = log2u(n);
+
+    DecArgs a;
+    std::memset(&a, 0, sizeof(a));
+    MapBuilder mb;
+    mb.build(a.orig, orig, K, off);
+    mb.build(a.rec, rec, R, off);
+    mb.build(a.out, work, K, off);
+    a.skew = ff16 ? c.t->skew16 : c.t->skew8;
+    a.tabs = ff16 ? c.t->tab16 : c.t->tab8;
+    a.zeros = c.t->zeros;
+    a.walsh = ff16 ? c.t->walsh16 : c.t->walsh8;
+    a.K = K;
+    a.R = R;
+    a.m = m;
+    a.Tn = Tn;
+
+    // error_locations[] = 1 at lost recoveries, [R, m), lost originals (LeopardFF8.cpp:1825-1840)
+    std::vector<uint32_t> erased((std::max(n, 256u) + 31) / 32, 0);
+    auto set = [&](unsigned p) { erased[p >> 5] |= 1u << (p & 31); };
+    for (unsigned i = 0; i < R; ++i)
+        if (!rec[i]) set(i);
+    for (unsigned i = R; i < m; ++i) set(i);
+    for (unsigned i = 0; i < K; ++i)
+        if (!orig[i]) set(m + i);
+
+    if (!ff16) {
+        std::memcpy(a.erased8, erased.data(), sizeof(a.erased8));
+        const size_t table_bytes = (mb.bytes() + 255) / 256 * 256;
+        LeopardResult r = c.ws->reserve_device(table_bytes);
+        if (r != Leopard_Success) return r;
+        r = mb.flush(*c.ws, reinterpret_cast<uint64_t*>(c.ws->dbuf), c.s);
+        if (r != Leopard_Success) return r;
+        a.nunits = bytes / 4;
+        HIP_OK(launch_decode_fused8(Tn, a, c.s), "decode kernel");
+        return Leopard_Success;
+    }
+
+    // FF16: erasure bitmap (full 65536 positions) + error locator on the device
+    const size_t bitmap_words = 65536 / 32;
+    const uint64_t slab_pieces = 3ull * n;
+    const uint64_t slice = mall_slice(bytes, slab_pieces);
+    const size_t table_bytes = (mb.bytes() + 255) / 256 * 256;
+    const size_t off_bitmap = table_bytes;
+    const size_t off_tmp = off_bitmap + bitmap_words * 4;
+    const size_t off_el = off_tmp + 65536 * 4;
+    const size_t off_slab = off_el + 65536 * 4;
+    LeopardResult r = c.ws->reserve_device(off_slab + slab_pieces * slice);
+    if (r != Leopard_Success) return r;
+    // stage tables + bitmap together
+    std::vector<uint32_t> bitmap(bitmap_words, 0);
+    std::copy(erased.begin(), erased.end(), bitmap.begin());
+    const size_t stage_bytes = table_bytes + bitmap_words * 4;
+    r = c.ws->reserve_stage(stage_bytes);
+    if (r != Leopard_Success) return r;
+    if (!mb.staged.empty()) std::memcpy(c.ws->hstage, mb.staged.data(), mb.bytes());
+    std::memcpy(c.ws->hstage + off_bitmap, bitmap.data(), bitmap_words * 4);
+    HIP_OK(hipMemcpyAsync(c.ws->dbuf, c.ws->hstage, stage_bytes, hipMemcpyHostToDevice, c.s), "upload decode state");
+    HIP_OK(hipEventRecord(c.ws->stage_done, c.s), "record staging");
+    c.ws->stage_pending = true;
+    for (auto& p : mb.pending) p.map->table = reinterpret_cast<uint64_t*>(c.ws->dbuf) + p.index;
+
+    uint32_t* d_bitmap = reinterpret_cast<uint32_t*>(c.ws->dbuf + off_bitmap);
+    uint32_t* d_tmp = reinterpret_cast<uint32_t*>(c.ws->dbuf + off_tmp);
+    uint32_t* d_el = reinterpret_cast<uint32_t*>(c.ws->dbuf + off_el);
+    HIP_OK(launch_error_locator16(d_bitmap, c.t->walsh16, d_tmp, d_el, c.s), "error locator");
+    a.el = d_el;
+    a.erased_dev = d_bitmap;
+    a.nlo = (m + K + (1u << kLoBits) - 1) >> kLoBits;
+
+    uint8_t* A = c.ws->dbuf + off_slab;
+    uint8_t* B = A + uint64_t(n) * slice;
+    uint8_t* Uu = B + uint64_t(n) * slice;
+    for (uint64_t pos = 0; pos < bytes; pos += slice) {
+        const uint64_t len = std::min(slice, bytes - pos);
+        DecArgs b = a;
+        b.orig.off = off + pos;
+        b.rec.off = off + pos;
+        b.out.off = off + pos;
+        b.nunits = len / 8;
+        b.a_out = PieceMap{nullptr, Uu, slice, 0};
+        HIP_OK(launch_decode_lo(b, c.s), "decode pass 1");
+        b.a_in = PieceMap{nullptr, Uu, slice, 0};
+        b.a_out = PieceMap{nullptr, A, slice, 0};
+        b.b_out = PieceMap{nullptr, B, slice, 0};
+        HIP_OK(launch_decode_hi(b, c.s), "decode pass 2");
+        b.a_in = PieceMap{nullptr, A, slice, 0};
+        b.b_in = PieceMap{nullptr, B, slice, 0};
+        HIP_OK(launch_decode_fin(b, c.s), "decode pass 3");
+    }
+    return Leopard_Success;
+}
+
+// ----------------------------------------------------- host-memory staging --
+
+// Host buffers: stage through device memory (reference contract: caller-owned
+// host pieces in, results in host memory on return).
+struct HostStage {
+    uint8_t* dev = nullptr;
+    size_t size = 0;
+    ~HostStage() {
+        if (dev) (void)hipFree(dev);
+    }
+};
+
+LeopardResult copy_pieces(hipStream_t s, void* const* dst, const void* const* src, unsigned count, uint64_t bytes,
+                          hipMemcpyKind kind) {
+    for (unsigned i = 0; i < count; ++i)
+        if (src[i] && dst[i]) HIP_OK(hipMemcpyAsync(dst[i], src[i], bytes, kind, s), "piece copy");
+    return Leopard_Success;
+}
+
+LeopardResult encode_any(uint64_t bytes, uint64_t off, unsigned K, unsigned R, const void* const* orig, void** work);
+LeopardResult decode_any(uint64_t bytes, uint64_t off, unsigned K, unsigned R, const void* const* orig,
+                         const void* const* rec, void** work);
+
+int pick_device(const void* first, MemKind* kind) {
+    int dev = -1;
+    *kind = classify(first, &dev);
+    if (*kind == MemKind::Device) return dev;
+    if (tls.device >= 0) return tls.device;
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    return cur;
+}
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        (void)hipGetDevice(&prev);
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        (void)hipGetDevice(&cur);
+        if (prev >= 0 && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+LeopardResult encode_any(uint64_t bytes, uint64_t off, unsigned K, unsigned R, const void* const* orig, void** work) {
+    MemKind kind;
+    const int dev = pick_device(orig[0], &kind);
+    DeviceGuard guard(dev);
+    Call c;
+    LeopardResult r = begin_call(dev, c);
+    if (r != Leopard_Success) return r;
+
+    if (kind == MemKind::Device) {
+        if (K == 1) {  // leopard.cpp:144-149
+            for (unsigned i = 0; i < R; ++i)
+                HIP_OK(hipMemcpyAsync(static_cast<uint8_t*>(work[i]) + off, static_cast<const uint8_t*>(orig[i]) + off,
+                                      bytes, hipMemcpyDeviceToDevice, c.s),
+                       "copy");
+        } else if (R == 1) {  // leopard.cpp:152-160
+            r = xor_device(c, bytes, off, orig, K, work[0]);
+        } else {
+            r = encode_device(c, bytes, off, K, R, orig, work);
+        }
+        if (r != Leopard_Success) return r;
+        return finish(c, false);
+    }
+
+    // host memory: stage K inputs + R outputs in a device slab
+    HostStage st;
+    HIP_OK(hipMalloc(reinterpret_cast<void**>(&st.dev), uint64_t(K + R) * bytes), "host staging");
+    std::vector<const void*> din(K), hsrc(K);
+    std::vector<void*> dout(R), hdst(R), ddst(K);
+    for (unsigned i = 0; i < K; ++i) {
+        din[i] = st.dev + uint64_t(i) * bytes;
+        ddst[i] = const_cast<void*>(din[i]);
+        hsrc[i] = static_cast<const uint8_t*>(orig[i]) + off;
+    }
+    for (unsigned i = 0; i < R; ++i) {
+        dout[i] = st.dev + uint64_t(K + i) * bytes;
+        hdst[i] = static_cast<uint8_t*>(work[i]) + off;
+    }
+    r = copy_pieces(c.s, ddst.data(), hsrc.data(), K, bytes, hipMemcpyHostToDevice);
+    if (r != Leopard_Success) return r;
+    if (K == 1) {
+        for (unsigned i = 0; i < R; ++i) dout[i] = const_cast<void*>(din[i]);
+    } else if (R == 1) {
+        r = xor_device(c, bytes, 0, din.data(), K, dout[0]);
+    } else {
+        r = encode_device(c, bytes, 0, K, R, din.data(), dout.data());
+    }
+    if (r != Leopard_Success) return r;
+    r = copy_pieces(c.s, hdst.data(), const_cast<const void* const*>(dout.data()), R, bytes, hipMemcpyDeviceToHost);
+    if (r != Leopard_Success) return r;
+    return finish(c, true);
+}
+
+LeopardResult decode_any(uint64_t bytes, uint64_t off, unsigned K, unsigned R, const void* const* orig,
+                         const void* const* rec, void** work) {
+    unsigned lost = 0, lost_i = 0, got = 0, got_i = 0;
+    for (unsigned i = 0; i < K; ++i)
+        if (!orig[i]) { ++lost; lost_i = i; }
+    for (unsigned i = 0; i < R; ++i)
+        if (rec[i]) { ++got; got_i = i; }
+    if (got < lost) return Leopard_NeedMoreData;  // leopard.cpp:275-276
+
+    const void* first = nullptr;
+    for (unsigned i = 0; i < K && !first; ++i) first = orig[i];
+    for (unsigned i = 0; i < R && !first; ++i) first = rec[i];
+    if (!first) first = work[0];
+    MemKind kind;
+    const int dev = pick_device(first, &kind);
+    DeviceGuard guard(dev);
+    Call c;
+    LeopardResult r = begin_call(dev, c);
+    if (r != Leopard_Success) return r;
+
+    // K == 1 copies recovery_data[last received] (leopard.cpp:279-283); with no
+    // recovery received the reference would read NULL, we copy the original.
+    const void* k1_src = K == 1 ? (rec[got_i] ? rec[got_i] : orig[0]) : nullptr;
+
+    if (kind == MemKind::Device) {
+        if (K == 1) {  // leopard.cpp:279-283
+            HIP_OK(hipMemcpyAsync(static_cast<uint8_t*>(work[0]) + off, static_cast<const uint8_t*>(k1_src) + off,
+                                  bytes, hipMemcpyDeviceToDevice, c.s),
+                   "copy");
+        } else if (lost == 0) {  // leopard.cpp:286-291
+            for (unsigned i = 0; i < K; ++i)
+                HIP_OK(hipMemcpyAsync(static_cast<uint8_t*>(work[i]) + off, static_cast<const uint8_t*>(orig[i]) + off,
+                                      bytes, hipMemcpyDeviceToDevice, c.s),
+                       "copy");
+        } else if (R == 1) {  // leopard.cpp:294-303
+            std::vector<const void*> src;
+            src.push_back(rec[0]);
+            for (unsigned i = 0; i < K; ++i)
+                if (orig[i]) src.push_back(orig[i]);
+            r = xor_device(c, bytes, off, src.data(), unsigned(src.size()), work[lost_i]);
+        } else {
+            r = decode_device(c, bytes, off, K, R, orig, rec, work);
+        }
+        if (r != Leopard_Success) return r;
+        return finish(c, false);
+    }
+
+    // host memory: present originals, present recoveries and the lost outputs
+    HostStage st;
+    HIP_OK(hipMalloc(reinterpret_cast<void**>(&st.dev), uint64_t(K + R) * bytes), "host staging");
+    std::vector<const void*> dorig(K, nullptr), drec(R, nullptr), hsrc;
+    std::vector<void*> dwork(K, nullptr), ddst, hdst;
+    for (unsigned i = 0; i < K; ++i) {
+        uint8_t* slot = st.dev + uint64_t(i) * bytes;
+        dwork[i] = slot;  // lost i is rebuilt in place of its original
+        if (orig[i]) {
+            dorig[i] = slot;
+            ddst.push_back(slot);
+            hsrc.push_back(static_cast<const uint8_t*>(orig[i]) + off);
+        }
+    }
+    for (unsigned i = 0; i < R; ++i) {
+        if (!rec[i]) continue;
+        uint8_t* slot = st.dev + uint64_t(K + i) * bytes;
+        drec[i] = slot;
+        ddst.push_back(slot);
+        hsrc.push_back(static_cast<const uint8_t*>(rec[i]) + off);
+    }
+    r = copy_pieces(c.s, ddst.data(), hsrc.data(), unsigned(ddst.size()), bytes, hipMemcpyHostToDevice);
+    if (r != Leopard_Success) return r;
+    std::vector<const void*> dres;
+    std::vector<void*> hout;
+    if (K == 1) {
+        dres.push_back(rec[got_i] ? drec[got_i] : dorig[0]);
+        hout.push_back(static_cast<uint8_t*>(work[0]) + off);
+    } else if (lost == 0) {
+        for (unsigned i = 0; i < K; ++i) {
+            dres.push_back(dorig[i]);
+            hout.push_back(static_cast<uint8_t*>(work[i]) + off);
+        }
+    } else if (R == 1) {
+        std::vector<const void*> src;
+        src.push_back(drec[0]);
+        for (unsigned i = 0; i < K; ++i)
+            if (dorig[i]) src.push_back(dorig[i]);
+        r = xor_device(c, bytes, 0, src.data(), unsigned(src.size()), dwork[lost_i]);
+        dres.push_back(dwork[lost_i]);
+        hout.push_back(static_cast<uint8_t*>(work[lost_i]) + off);
+    } else {
+        r = decode_device(c, bytes, 0, K, R, dorig.data(), drec.data(), dwork.data());
+        for (unsigned i = 0; i < K; ++i)
+            if (!orig[i]) {
+                dres.push_back(dwork[i]);
+                hout.push_back(static_cast<uint8_t*>(work[i]) + off);
+            }
+    }
+    if (r != Leopard_Success) return r;
+    r = copy_pieces(c.s, hout.data(), dres.data(), unsigned(dres.size()), bytes, hipMemcpyDeviceToHost);
+    if (r != Leopard_Success) return r;
+    return finish(c, true);
+}
+
+// Validation shared by leo_encode / leo_amd_encode_slice (leopard.cpp:131-140, 162-166).
+LeopardResult check_encode(uint64_t bytes, unsigned K, unsigned R, unsigned work_count, const void* const* orig,
+                           void** work) {
+    if (bytes == 0 || bytes % 64 != 0) return Leopard_InvalidSize;
+    if (R == 0 || R > K) return Leopard_InvalidCounts;
+    if (!orig || !work) return Leopard_InvalidInput;
+    if (!g_initialized) return Leopard_CallInitialize;
+    if (K == 1 || R == 1) return Leopard_Success;
+    const unsigned m = next_pow2(R);
+    const unsigned n = next_pow2(m + K);
+    if (work_count != m * 2) return Leopard_InvalidCounts;
+    if (n > 65536) return Leopard_TooMuchData;
+    return Leopard_Success;
+}
+
+// leopard.cpp:242-252, 305-309 (NeedMoreData is decided later, after counting).
+LeopardResult check_decode(uint64_t bytes, unsigned K, unsigned R, unsigned work_count, const void* const* orig,
+                           const void* const* rec, void** work) {
+    if (bytes == 0 || bytes % 64 != 0) return Leopard_InvalidSize;
+    if (R == 0 || R > K) return Leopard_InvalidCounts;
+    if (!orig || !rec || !work) return Leopard_InvalidInput;
+    if (!g_initialized) return Leopard_CallInitialize;
+    return Leopard_Success;
+}
+
+LeopardResult decode_checked(uint64_t bytes, uint64_t off, unsigned K, unsigned R, unsigned work_count,
+                             const void* const* orig, const void* const* rec, void** work) {
+    // the general path needs work_count == n (leopard.cpp:305-309); edge paths do not
+    unsigned lost = 0, got = 0;
+    for (unsigned i = 0; i < K; ++i) lost += orig[i] == nullptr;
+    for (unsigned i = 0; i < R; ++i) got += rec[i] != nullptr;
+    if (got < lost) return Leopard_NeedMoreData;
+    if (K != 1 && lost != 0 && R != 1) {
+        const unsigned m = next_pow2(R);
+        const unsigned n = next_pow2(m + K);
+        if (work_count != n) return Leopard_InvalidCounts;
+        if (n > 65536) return Leopard_TooMuchData;
+    }
+    return decode_any(bytes, off, K, R, orig, rec, work);
+}
+
+}  // namespace
+}  // namespace lamd
+
+using namespace lamd;
+
+extern "C" {
+
+LEO_EXPORT int leo_init_(int version) {
+    if (version != LEO_VERSION) return Leopard_InvalidInput;
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_initialized) return Leopard_Success;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
+        (void)hipGetLastError();
+        tls.last_error = "no HIP device visible";
+        return Leopard_Platform;
+    }
+    for (int d = 0; d < count; ++d) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, d) != hipSuccess) return Leopard_Platform;
+        if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+            tls.last_error = std::string("unsupported GPU architecture ") + prop.gcnArchName;
+            return Leopard_Platform;
+        }
+    }
+    const GaloisField& f8 = field8();
+    const GaloisField& f16 = field16();
+    build_perm_tables8(f8, g_h_tab8);
+    build_perm_tables16(f16, g_h_tab16);
+    g_h_skew8.assign(f8.skew.begin(), f8.skew.end());
+    g_h_skew8.push_back(0);
+    g_h_skew16.assign(f16.skew.begin(), f16.skew.end());
+    g_h_skew16.push_back(0);
+    g_h_walsh8.assign(f8.log_walsh.begin(), f8.log_walsh.end());
+    g_h_walsh16.assign(f16.log_walsh.begin(), f16.log_walsh.end());
+    g_dev.assign(count, DeviceTables{});
+    g_device_count = count;
+    g_initialized = true;
+    return Leopard_Success;
+}
+
+LEO_EXPORT const char* leo_result_string(LeopardResult result) {
+    switch (result) {
+        case Leopard_Success: return "Operation succeeded";
+        case Leopard_NeedMoreData: return "Not enough recovery data received";
+        case Leopard_TooMuchData: return "Buffer counts are too high";
+        case Leopard_InvalidSize: return "Buffer size must be a multiple of 64 bytes";
+        case Leopard_InvalidCounts: return "Invalid counts provided";
+        case Leopard_InvalidInput: return "A function parameter was invalid";
+        case Leopard_Platform: return "Platform is unsupported";
+        case Leopard_CallInitialize: return "Call leo_init() first";
+    }
+    return "Unknown";
+}
+
+LEO_EXPORT unsigned leo_encode_work_count(unsigned original_count, unsigned recovery_count) {
+    if (original_count == 1) return recovery_count;
+    if (recovery_count == 1) return 1;
+    return next_pow2(recovery_count) * 2;
+}
+
+LEO_EXPORT unsigned leo_decode_work_count(unsigned original_count, unsigned recovery_count) {
+    if (original_count == 1 || recovery_count == 1) return original_count;
+    const unsigned m = next_pow2(recovery_count);
+    return next_pow2(m + original_count);
+}
+
+LEO_EXPORT LeopardResult leo_encode(uint64_t buffer_bytes, unsigned original_count, unsigned recovery_count,
+                                    unsigned work_count, const void* const* const original_data, void** work_data) {
+    LeopardResult r = check_encode(buffer_bytes, original_count, recovery_count, work_count, original_data, work_data);
+    if (r != Leopard_Success) return r;
+    return encode_any(buffer_bytes, 0, original_count, recovery_count, original_data, work_data);
+}
+
+LEO_EXPORT LeopardResult leo_decode(uint64_t buffer_bytes, unsigned original_count, unsigned recovery_count,
+                                    unsigned work_count, const void* const* const original_data,
+                                    const void* const* const recovery_data, void** work_data) {
+    LeopardResult r = check_decode(buffer_bytes, original_count, recovery_count, work_count, original_data,
+                                   recovery_data, work_data);
+    if (r != Leopard_Success) return r;
+    return decode_checked(buffer_bytes, 0, original_count, recovery_count, work_count, original_data, recovery_data,
+                          work_data);
+}
+
+LEO_EXPORT LeopardResult leo_amd_encode_slice(uint64_t buffer_bytes, uint64_t byte_offset, uint64_t slice_bytes,
+                                              unsigned original_count, unsigned recovery_count, unsigned work_count,
+                                              const void* const* const original_data, void** work_data) {
+    if (slice_bytes == 0 || slice_bytes % 64 || byte_offset % 64 || byte_offset + slice_bytes > buffer_bytes)
+        return Leopard_InvalidSize;
+    LeopardResult r = check_encode(buffer_bytes, original_count, recovery_count, work_count, original_data, work_data);
+    if (r != Leopard_Success) return r;
+    return encode_any(slice_bytes, byte_offset, original_count, recovery_count, original_data, work_data);
+}
+
+LEO_EXPORT LeopardResult leo_amd_decode_slice(uint64_t buffer_bytes, uint64_t byte_offset, uint64_t slice_bytes,
+                                              unsigned original_count, unsigned recovery_count, unsigned work_count,
+                                              const void* const* const original_data,
+                                              const void* const* const recovery_data, void** work_data) {
+    if (slice_bytes == 0 || slice_bytes % 64 || byte_offset % 64 || byte_offset + slice_bytes > buffer_bytes)
+        return Leopard_InvalidSize;
+    LeopardResult r = check_decode(buffer_bytes, original_count, recovery_count, work_count, original_data,
+                                   recovery_data, work_data);
+    if (r != Leopard_Success) return r;
+    return decode_checked(slice_bytes, byte_offset, original_count, recovery_count, work_count, original_data,
+                          recovery_data, work_data);
+}
+
+LEO_EXPORT void leo_amd_set_stream(void* hip_stream) { tls.stream = static_cast<hipStream_t>(hip_stream); }
+LEO_EXPORT void leo_amd_set_async(int async_enable) { tls.async = async_enable != 0; }
+LEO_EXPORT void leo_amd_set_device(int device) { tls.device = device; }
+
+LEO_EXPORT int leo_amd_device_count(void) {
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return count;
+}
+
+LEO_EXPORT int leo_amd_table(int field, int which, uint16_t* out, unsigned capacity) {
+    if ((field != 8 && field != 16) || which < 0 || which > 3 || !out) return Leopard_InvalidInput;
+    const GaloisField& f = field == 8 ? field8() : field16();
+    const std::vector<uint16_t>& v = which == 0 ? f.log_of : which == 1 ? f.exp_of : which == 2 ? f.skew : f.log_walsh;
+    std::memcpy(out, v.data(), std::min<size_t>(capacity, v.size()) * sizeof(uint16_t));
+    return int(v.size());
+}
+
+LEO_EXPORT const char* leo_amd_last_error(void) { return tls.last_error.c_str(); }
+
+}  // extern "C"

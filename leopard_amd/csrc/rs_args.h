@@ -1,0 +1,64 @@
+// rs_args.h -- kernel argument blocks shared by the host dispatcher and kernels.
+#pragma once
+
+#include <cstdint>
+
+#include "rs_device.h"
+
+namespace lamd {
+
+// Tile bits of the "low" passes of a multi-pass FF16 transform (2^8 pieces per
+// workgroup tile; the remaining high bits form the second tile).
+constexpr unsigned kLoBits = 8;
+
+struct EncArgs {
+    PieceMap in;        // originals (K)
+    PieceMap out;       // recovery destinations (R)
+    PieceMap slab_in;   // multi-pass intermediate read
+    PieceMap slab_out;  // multi-pass intermediate write
+    const uint32_t* skew;
+    const uint32_t* tabs;   // multiply tables; entry kModulus+1 is all zero
+    const uint8_t* zeros;   // >= 256 zero bytes
+    unsigned K, R, Tm, nchunks;
+    uint64_t nunits;  // column units in this launch
+};
+
+struct DecArgs {
+    PieceMap orig, rec, out;
+    PieceMap a_in, b_in, a_out, b_out;  // multi-pass intermediates
+    const uint32_t* skew;
+    const uint32_t* tabs;
+    const uint8_t* zeros;
+    const uint32_t* walsh;       // FF8: LogWalsh for the in-kernel error locator
+    const uint32_t* el;          // FF16: precomputed error locator logs
+    const uint32_t* erased_dev;  // FF16: erasure bitmap over positions [0, n)
+    uint32_t erased8[8];         // FF8: erasure bitmap by value
+    unsigned K, R, m, Tn, nlo;   // nlo: number of non-zero low tiles
+    uint64_t nunits;
+};
+
+struct XorArgs {
+    PieceMap src;
+    unsigned count;
+    PieceMap out;
+    uint64_t ndwords;
+};
+
+// Launchers (rs_kernels.hip).  Return hipSuccess or the launch error.
+hipError_t launch_encode_fused(int ff16, unsigned T, const EncArgs& a, hipStream_t s);
+hipError_t launch_encode_lo(const EncArgs& a, hipStream_t s);
+hipError_t launch_encode_hi(const EncArgs& a, hipStream_t s);
+hipError_t launch_encode_fin(const EncArgs& a, hipStream_t s);
+hipError_t launch_decode_fused8(unsigned T, const DecArgs& a, hipStream_t s);
+hipError_t launch_decode_lo(const DecArgs& a, hipStream_t s);
+hipError_t launch_decode_hi(const DecArgs& a, hipStream_t s);
+hipError_t launch_decode_fin(const DecArgs& a, hipStream_t s);
+hipError_t launch_error_locator16(const uint32_t* erased, const uint32_t* walsh, uint32_t* tmp, uint32_t* el,
+                                  hipStream_t s);
+hipError_t launch_xor_reduce(const XorArgs& a, hipStream_t s);
+
+// Units per lane chosen for each kernel family (the host sizes grids with it).
+constexpr int kUnitsPerLane = 1;
+constexpr unsigned kUnitsPerTile = 64 * kUnitsPerLane;
+
+}  // namespace lamd

@@ -1,0 +1,551 @@
+// rs_kernels.hip -- the Reed-Solomon encode/decode kernels for gfx950.
+//
+// Encoder (reference ReedSolomonEncode, LeopardFF8.cpp:1602-1672):
+//   work = XOR_c IFFT_m(data[c*m .. c*m+m), skew + m-1 + c*m);  out = FFT_m(work, skew - 1)[0..R)
+// Decoder (reference ReedSolomonDecode, LeopardFF8.cpp:1809-1916):
+//   el   = FWHT(LogWalsh * FWHT(erasures))          error locator, as logs
+//   v    = IFFT_n(el * received, skew - 1)
+//   z    = FormalDerivative(v)
+//   lost original i = FFT_n(z)[m + i] * exp(-el[m + i])
+//
+// Kernel families (T = tile bits, see rs_device.h):
+//   k_enc_fused / k_dec_fused : the whole transform in one workgroup tile
+//                               (FF8: m <= 128, n <= 256; FF16 encode m <= 256)
+//   k_enc_lo/hi/fin, k_dec_lo/hi/fin : FF16 transforms of 2^9 .. 2^16 pieces as
+//     three tile passes: low 8 bits, high bits, low 8 bits again.  The formal
+//     derivative is split between the passes with
+//        F_lo F_hi (I + D_hi + D_lo) v = F_lo ( F_hi (I + D_hi) v  +  D_lo F_hi v ),
+//     valid because D_lo (flips of low bits) commutes with every butterfly of
+//     the high layers, whose skew depends only on the high bits of the index.
+#include <hip/hip_runtime.h>
+
+#include "rs_args.h"
+
+namespace lamd {
+
+namespace {
+
+constexpr int C = kUnitsPerLane;
+
+constexpr int wave_bits(int T) { return T <= 4 ? 0 : T - 4; }
+
+template <class F, int T>
+constexpr size_t tile_lds_bytes() {
+    return wave_bits(T) > 0 ? (size_t(1) << T) * 64 * C * F::kDw * 4 : 0;
+}
+
+LDEV uint64_t lane_units(unsigned lane) { return (uint64_t(blockIdx.x) * 64 + lane) * C; }
+
+// Piece i of pm when `ok` (wave-uniform), else zeros read from the zero page.
+// The choice is made on scalars so the vector code has no branch.
+template <class F>
+LDEV void load_or_zero(uint32_t* x, const PieceMap& pm, bool ok, unsigned i, const uint8_t* zeros, uint64_t q) {
+    const uint8_t* src = zeros;
+    uint64_t qq = 0;
+    if (ok) { src = pm.ptr(i); qq = q; }
+    load_units<F, C>(x, src, qq);
+}
+
+// ------------------------------------------------------------------ encode --
+
+template <class F, int T>
+__global__ void __launch_bounds__(64 << wave_bits(T)) k_enc_fused(EncArgs a) {
+    constexpr int H = wave_bits(T);
+    using TL = Tile<F, T, H, C>;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const uint64_t q0 = lane_units(lane);
+    const bool live = q0 < a.nunits;
+    const uint64_t ql = live ? q0 : a.nunits - C;  // dead lanes re-read a valid unit: loads stay unpredicated
+    constexpr unsigned m = 1u << T;
+    const PieceSpace ps{0, 0, 0};
+    typename TL::Reg acc, x;
+    for (unsigned c = 0; c < a.nchunks; ++c) {
+        const unsigned base = c * m;
+        const unsigned cnt = a.K - base < m ? a.K - base : m;
+#pragma unroll
+        for (int r = 0; r < TL::NR; ++r) {
+            const unsigned tp = TL::piece(0, r, w);
+            load_or_zero<F>(x[r], a.in, tp < cnt, base + tp, a.zeros, ql);
+        }
+        TL::ifft(x, w, lane, lds, ps, a.skew + (m - 1 + base), a.tabs);
+        if (c == 0) TL::copy(acc, x);
+        else TL::xor_into(acc, x);
+    }
+    TL::fft(acc, w, lane, lds, ps, a.skew - 1, a.tabs);
+#pragma unroll
+    for (int r = 0; r < TL::NR; ++r) {
+        const unsigned tp = TL::piece(0, r, w);
+        if (tp < a.R && live) store_units<F, C>(a.out.ptr(tp), q0, acc[r]);
+    }
+}
+
+// pass 1: IFFT over the low kLoBits of chunk blockIdx.z -> slab_out[c*m + g]
+template <class F>
+__global__ void __launch_bounds__(64 << wave_bits(kLoBits)) k_enc_lo(EncArgs a) {
+    constexpr int T = kLoBits, H = wave_bits(T);
+    using TL = Tile<F, T, H, C>;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const uint64_t q0 = lane_units(lane);
+    const bool live = q0 < a.nunits;
+    const uint64_t ql = live ? q0 : a.nunits - C;  // dead lanes re-read a valid unit: loads stay unpredicated
+    const unsigned m = 1u << a.Tm;
+    const unsigned c = blockIdx.z, base = c * m;
+    const PieceSpace ps{0, 0, blockIdx.y << T};
+    typename TL::Reg x;
+#pragma unroll
+    for (int r = 0; r < TL::NR; ++r) {
+        const unsigned g = ps.global(TL::piece(0, r, w));
+        load_or_zero<F>(x[r], a.in, base + g < a.K, base + g, a.zeros, ql);
+    }
+    TL::ifft(x, w, lane, lds, ps, a.skew + (m - 1 + base), a.tabs);
+    if (!live) return;
+#pragma unroll
+    for (int r = 0; r < TL::NR; ++r) {
+        const unsigned g = ps.global(TL::piece(1, r, w));
+        store_units<F, C>(a.slab_out.ptr(base + g), q0, x[r]);
+    }
+}
+
+// pass 2: for every chunk IFFT over the high bits and accumulate; then the
+// FFT over the high bits -> slab_out[g]
+template <class F, int T>
+__global__ void __launch_bounds__(64 << wave_bits(T)) k_enc_hi(EncArgs a) {
+    constexpr int H = wave_bits(T);
+    using TL = Tile<F, T, H, C>;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const uint64_t q0 = lane_units(lane);
+    const bool live = q0 < a.nunits;
+    const uint64_t ql = live ? q0 : a.nunits - C;  // dead lanes re-read a valid unit: loads stay unpredicated
+    const unsigned m = 1u << a.Tm;
+    const PieceSpace ps{blockIdx.y, kLoBits, 0};
+    typename TL::Reg acc, x;
+    for (unsigned c = 0; c < a.nchunks; ++c) {
+        const unsigned base = c * m;
+#pragma unroll
+        for (int r = 0; r < TL::NR; ++r) {
+            const unsigned tp = TL::piece(0, r, w);
+            const unsigned g = ps.global(tp);
+            // low tiles that lie entirely past K were all-zero inputs
+            load_or_zero<F>(x[r], a.slab_in, base + (tp << kLoBits) < a.K, base + g, a.zeros, ql);
+        }
+        TL::ifft(x, w, lane, lds, ps, a.skew + (m - 1 + base), a.tabs);
+        if (c == 0) TL::copy(acc, x);
+        else TL::xor_into(acc, x);
+    }
+    TL::fft(acc, w, lane, lds, ps, a.skew - 1, a.tabs);
+    if (!live) return;
+#pragma unroll
+    for (int r = 0; r < TL::NR; ++r) {
+        const unsigned g = ps.global(TL::piece(0, r, w));
+        store_units<F, C>(a.slab_out.ptr(g), q0, acc[r]);
+    }
+}
+
+// pass 3: FFT over the low bits, keep outputs g < R
+template <class F>
+__global__ void __launch_bounds__(64 << wave_bits(kLoBits)) k_enc_fin(EncArgs a) {
+    constexpr int T = kLoBits, H = wave_bits(T);
+    using TL = Tile<F, T, H, C>;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const uint64_t q0 = lane_units(lane);
+    const bool live = q0 < a.nunits;
+    const uint64_t ql = live ? q0 : a.nunits - C;  // dead lanes re-read a valid unit: loads stay unpredicated
+    const PieceSpace ps{0, 0, blockIdx.y << T};
+    typename TL::Reg x;
+#pragma unroll
+    for (int r = 0; r < TL::NR; ++r) {
+        const unsigned g = ps.global(TL::piece(1, r, w));
+        load_units<F, C>(x[r], a.slab_in.ptr(g), ql);
+    }
+    TL::fft(x, w, lane, lds, ps, a.skew - 1, a.tabs);
+    if (!live) return;
+#pragma unroll
+    for (int r = 0; r < TL::NR; ++r) {
+        const unsigned g = ps.global(TL::piece(0, r, w));
+        if (g < a.R) store_units<F, C>(a.out.ptr(g), q0, x[r]);
+    }
+}
+
+// ------------------------------------------------------------------ decode --
+
+LDEV bool bit_set(const uint32_t* bits, unsigned p) { return (cload(bits + (p >> 5)) >> (p & 31)) & 1u; }
+
+// Erasure bitmap over codeword positions (bit p <=> error_locations[p] = 1,
+// LeopardFF8.cpp:1825-1840): FF8 passes it by value, FF16 in device memory.
+struct Erased8 {
+    uint32_t w[8];
+    LDEV bool get(unsigned p) const {
+        const unsigned i = p >> 5;
+        uint32_t v = w[0];
+#pragma unroll
+        for (unsigned k = 1; k < 8; ++k) v = i == k ? w[k] : v;
+        return (v >> (p & 31)) & 1u;
+    }
+};
+struct ErasedDev {
+    const uint32_t* bits;
+    LDEV bool get(unsigned p) const { return bit_set(bits, p); }
+};
+
+// FF8 error locator inside the kernel: each wave evaluates all 256 entries,
+// lane holding positions lane + 64 j (LeopardFF8.cpp:1848-1853).  Fully reduced
+// mod 255 (congruent to the reference's partially reduced values; the
+// multiply tables treat 0 and 255 identically).
+struct El8 {
+    unsigned e[4];
+    LDEV static unsigned addm(unsigned a, unsigned b) { unsigned s = a + b; return s >= 255u ? s - 255u : s; }
+    LDEV static unsigned subm(unsigned a, unsigned b) { unsigned s = a + 255u - b; return s >= 255u ? s - 255u : s; }
+    LDEV void fwht(unsigned lane) {
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const unsigned o = __shfl_xor(int(e[j]), d);
+                e[j] = (lane & d) ? subm(o, e[j]) : addm(e[j], o);
+            }
+        }
+        const unsigned a0 = addm(e[0], e[1]), a1 = subm(e[0], e[1]);
+        const unsigned a2 = addm(e[2], e[3]), a3 = subm(e[2], e[3]);
+        e[0] = addm(a0, a2); e[2] = subm(a0, a2);
+        e[1] = addm(a1, a3); e[3] = subm(a1, a3);
+    }
+    LDEV void compute(const Erased8& er, const uint32_t* __restrict__ walsh, unsigned lane) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) e[j] = er.get(lane + 64 * j);
+        fwht(lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) e[j] = (e[j] * walsh[lane + 64 * j]) % 255u;
+        fwht(lane);
+    }
+    LDEV unsigned at(unsigned p) const {  // p wave-uniform
+        const unsigned j = p >> 6;
+        const unsigned v = j == 0 ? e[0] : j == 1 ? e[1] : j == 2 ? e[2] : e[3];
+        return __builtin_amdgcn_readlane(v, p & 63);
+    }
+};
+struct ElDev {
+    const uint32_t* el;
+    LDEV unsigned at(unsigned p) const { return cload(el + p); }
+};
+
+// Received piece at codeword position p, scaled by exp(el[p]); zero if absent.
+// Positions: [0, m) recovery (only [0, R) exist), [m, m+K) originals
+// (LeopardFF8.cpp:1857-1877).  Branch-free on the vector side: an absent piece
+// reads the zero page at unit 0 through the all-zero multiply table.
+template <class F, class Er, class El>
+LDEV void load_received(uint32_t* x, const DecArgs& a, const Er& erased, const El& el, unsigned p, uint64_t q) {
+    const uint8_t* src = a.zeros;
+    unsigned lm = F::kModulus + 1;  // the zero table
+    uint64_t qq = 0;
+    if (!erased.get(p)) {
+        if (p < a.R) { src = a.rec.ptr(p); lm = el.at(p); qq = q; }
+        else if (p >= a.m && p < a.m + a.K) { src = a.orig.ptr(p - a.m); lm = el.at(p); qq = q; }
+    }
+    uint32_t y[C * F::kDw];
+    load_units<F, C>(y, src, qq);
+    const typename F::Tab t = F::tab(a.tabs, lm);
+#pragma unroll
+    for (int u = 0; u < C; ++u) F::mul(&x[u * F::kDw], &y[u * F::kDw], t);
+}
+
+// Lost original at position p = m + i: work[i] = z[p] * exp(-el[p])  (LeopardFF8.cpp:1913-1915).
+template <class F, class Er, class El>
+LDEV void reveal(const uint32_t* z, const DecArgs& a, const Er& erased, const El& el, unsigned p, uint64_t q0) {
+    if (p >= a.m && p < a.m + a.K && erased.get(p)) {
+        uint32_t y[C * F::kDw];
+        const typename F::Tab t = F::tab(a.tabs, F::kModulus - el.at(p));
+#pragma unroll
+        for (int u = 0; u < C; ++u) F::mul(&y[u * F::kDw], &z[u * F::kDw], t);
+        store_units<F, C>(a.out.ptr(p - a.m), q0, y);
+    }
+}
+
+template <class F, int T>
+__global__ void __launch_bounds__(64 << wave_bits(T)) k_dec_fused(DecArgs a) {
+    constexpr int H = wave_bits(T);
+    using TL = Tile<F, T, H, C>;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const uint64_t q0 = lane_units(lane);
+    const bool live = q0 < a.nunits;
+    const uint64_t ql = live ? q0 : a.nunits - C;  // dead lanes re-read a valid unit: loads stay unpredicated
+    const PieceSpace ps{0, 0, 0};
+    Erased8 erased;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) erased.w[k] = a.erased8[k];
+    El8 el;
+    el.compute(erased, a.walsh, lane);
+
+    typename TL::Reg v, z;
+#pragma unroll
+    for (int r = 0; r < TL::NR; ++r) load_received<F>(v[r], a, erased, el, TL::piece(0, r, w), ql);
+    TL::ifft(v, w, lane, lds, ps, a.skew - 1, a.tabs);
+    TL::copy(z, v);
+    TL::derivative_add(z, v, w, lane, lds);
+    TL::fft(z, w, lane, lds, ps, a.skew - 1, a.tabs);
+    if (!live) return;
+#pragma unroll
+    for (int r = 0; r < TL::NR; ++r) reveal<F>(z[r], a, erased, el, TL::piece(0, r, w), q0);
+}
+
+// pass 1: scale-on-load + IFFT over the low bits -> a_out[g]
+template <class F>
+__global__ void __launch_bounds__(64 << wave_bits(kLoBits)) k_dec_lo(DecArgs a) {
+    constexpr int T = kLoBits, H = wave_bits(T);
+    using TL = Tile<F, T, H, C>;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const uint64_t q0 = lane_units(lane);
+    const bool live = q0 < a.nunits;
+    const uint64_t ql = live ? q0 : a.nunits - C;  // dead lanes re-read a valid unit: loads stay unpredicated
+    const PieceSpace ps{0, 0, blockIdx.y << T};
+    const ErasedDev erased{a.erased_dev};
+    const ElDev el{a.el};
+    typename TL::Reg v;
+#pragma unroll
+    for (int r = 0; r < TL::NR; ++r) load_received<F>(v[r], a, erased, el, ps.global(TL::piece(0, r, w)), ql);
+    TL::ifft(v, w, lane, lds, ps, a.skew - 1, a.tabs);
+    if (!live) return;
+#pragma unroll
+    for (int r = 0; r < TL::NR; ++r) store_units<F, C>(a.a_out.ptr(ps.global(TL::piece(1, r, w))), q0, v[r]);
+}
+
+// pass 2: IFFT over the high bits, a = (I + D_hi) v, write F_hi(a), F_hi(v)
+template <class F, int T>
+__global__ void __launch_bounds__(64 << wave_bits(T)) k_dec_hi(DecArgs a) {
+    constexpr int H = wave_bits(T);
+    using TL = Tile<F, T, H, C>;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const uint64_t q0 = lane_units(lane);
+    const bool live = q0 < a.nunits;
+    const uint64_t ql = live ? q0 : a.nunits - C;  // dead lanes re-read a valid unit: loads stay unpredicated
+    const PieceSpace ps{blockIdx.y, kLoBits, 0};
+    typename TL::Reg v, d;
+#pragma unroll
+    for (int r = 0; r < TL::NR; ++r) {
+        const unsigned tp = TL::piece(0, r, w);
+        load_or_zero<F>(v[r], a.a_in, tp < a.nlo, ps.global(tp), a.zeros, ql);
+    }
+    TL::ifft(v, w, lane, lds, ps, a.skew - 1, a.tabs);
+    TL::copy(d, v);
+    TL::derivative_add(d, v, w, lane, lds);
+    TL::fft(d, w, lane, lds, ps, a.skew - 1, a.tabs);
+    if (live)
+#pragma unroll
+        for (int r = 0; r < TL::NR; ++r) store_units<F, C>(a.a_out.ptr(ps.global(TL::piece(0, r, w))), q0, d[r]);
+    TL::fft(v, w, lane, lds, ps, a.skew - 1, a.tabs);
+    if (live)
+#pragma unroll
+        for (int r = 0; r < TL::NR; ++r) store_units<F, C>(a.b_out.ptr(ps.global(TL::piece(0, r, w))), q0, v[r]);
+}
+
+// pass 3: z = A + D_lo(V), FFT over the low bits, reveal lost originals
+template <class F>
+__global__ void __launch_bounds__(64 << wave_bits(kLoBits)) k_dec_fin(DecArgs a) {
+    constexpr int T = kLoBits, H = wave_bits(T);
+    using TL = Tile<F, T, H, C>;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const uint64_t q0 = lane_units(lane);
+    const bool live = q0 < a.nunits;
+    const uint64_t ql = live ? q0 : a.nunits - C;  // dead lanes re-read a valid unit: loads stay unpredicated
+    const PieceSpace ps{0, 0, blockIdx.y << T};
+    // skip tiles holding no lost original (uniform across the workgroup)
+    {
+        const unsigned g0 = blockIdx.y << T;
+        unsigned any = 0;
+        for (unsigned i = g0 >> 5; i < (g0 + (1u << T)) >> 5; ++i) any |= cload(a.erased_dev + i);
+        const unsigned lo = a.m, hi = a.m + a.K;
+        if (!any || g0 + (1u << T) <= lo || g0 >= hi) return;
+    }
+    const ErasedDev erased{a.erased_dev};
+    const ElDev el{a.el};
+    typename TL::Reg z, v;
+#pragma unroll
+    for (int r = 0; r < TL::NR; ++r) {
+        const unsigned g = ps.global(TL::piece(1, r, w));
+        load_units<F, C>(z[r], a.a_in.ptr(g), ql);
+        load_units<F, C>(v[r], a.b_in.ptr(g), ql);
+    }
+    TL::derivative_add(z, v, w, lane, lds);
+    TL::fft(z, w, lane, lds, ps, a.skew - 1, a.tabs);
+    if (!live) return;
+#pragma unroll
+    for (int r = 0; r < TL::NR; ++r) reveal<F>(z[r], a, erased, el, ps.global(TL::piece(0, r, w)), q0);
+}
+
+// FF16 error locator over 65536 positions as a 256 x 256 Walsh-Hadamard
+// transform: rows (low 8 bits) / columns (high 8 bits), one wave per line.
+struct Mod16 {
+    LDEV static unsigned add(unsigned a, unsigned b) { unsigned s = a + b; return s >= 65535u ? s - 65535u : s; }
+    LDEV static unsigned sub(unsigned a, unsigned b) { unsigned s = a + 65535u - b; return s >= 65535u ? s - 65535u : s; }
+};
+LDEV void fwht256(unsigned (&e)[4], unsigned lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const unsigned o = __shfl_xor(int(e[j]), d);
+            e[j] = (lane & d) ? Mod16::sub(o, e[j]) : Mod16::add(e[j], o);
+        }
+    const unsigned a0 = Mod16::add(e[0], e[1]), a1 = Mod16::sub(e[0], e[1]);
+    const unsigned a2 = Mod16::add(e[2], e[3]), a3 = Mod16::sub(e[2], e[3]);
+    e[0] = Mod16::add(a0, a2); e[2] = Mod16::sub(a0, a2);
+    e[1] = Mod16::add(a1, a3); e[3] = Mod16::sub(a1, a3);
+}
+
+// mode 0: rows of the erasure bitmap -> tmp; mode 1: rows of tmp -> el (u16)
+__global__ void __launch_bounds__(64) k_el16_rows(const uint32_t* erased, uint32_t* tmp, uint32_t* el, int mode) {
+    const unsigned lane = threadIdx.x, row = blockIdx.x;
+    unsigned e[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const unsigned p = row * 256 + lane + 64 * j;
+        e[j] = mode == 0 ? bit_set(erased, p) : tmp[p];
+    }
+    fwht256(e, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const unsigned p = row * 256 + lane + 64 * j;
+        if (mode == 0) tmp[p] = e[j];
+        else el[p] = e[j];
+    }
+}
+// columns: FWHT over the high bits, pointwise * LogWalsh mod 65535, FWHT again
+__global__ void __launch_bounds__(64) k_el16_cols(uint32_t* tmp, const uint32_t* walsh) {
+    const unsigned lane = threadIdx.x, col = blockIdx.x;
+    unsigned e[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) e[j] = tmp[col + 256 * (lane + 64 * j)];
+    fwht256(e, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const unsigned p = col + 256 * (lane + 64 * j);
+        e[j] = (e[j] * walsh[p]) % 65535u;
+    }
+    fwht256(e, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) tmp[col + 256 * (lane + 64 * j)] = e[j];
+}
+
+// R == 1 parity paths (leopard.cpp:106-121, 214-231): out = XOR of pieces.
+__global__ void __launch_bounds__(256) k_xor_reduce(XorArgs a) {
+    const uint64_t q = (uint64_t(blockIdx.x) * 256 + threadIdx.x) * 4;  // dword index
+    if (q >= a.ndwords) return;
+    uint4 acc = make_uint4(0, 0, 0, 0);
+    for (unsigned i = 0; i < a.count; ++i) {
+        const uint8_t* p = a.src.ptr(i);
+        const uint4 v = *reinterpret_cast<const uint4*>(p + q * 4);
+        acc.x ^= v.x; acc.y ^= v.y; acc.z ^= v.z; acc.w ^= v.w;
+    }
+    *reinterpret_cast<uint4*>(a.out.ptr(0) + q * 4) = acc;
+}
+
+// ------------------------------------------------------------ dispatching --
+
+unsigned tiles_for(uint64_t nunits) { return unsigned((nunits + kUnitsPerTile - 1) / kUnitsPerTile); }
+
+template <class KernelFn>
+hipError_t launch(KernelFn* fn, dim3 grid, unsigned threads, size_t lds, hipStream_t s, const void* args_ptr,
+                  size_t args_size) {
+    if (lds > 65536) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+        if (e != hipSuccess) return e;
+    }
+    (void)args_size;
+    void* params[] = {const_cast<void*>(args_ptr)};
+    return hipLaunchKernel(reinterpret_cast<const void*>(fn), grid, dim3(threads), params, lds, s);
+}
+
+template <class F, int T>
+hipError_t enc_fused_t(const EncArgs& a, hipStream_t s) {
+    return launch(&k_enc_fused<F, T>, dim3(tiles_for(a.nunits)), 64u << wave_bits(T), tile_lds_bytes<F, T>(), s, &a,
+                  sizeof(a));
+}
+template <class F, int T>
+hipError_t dec_fused_t(const DecArgs& a, hipStream_t s) {
+    return launch(&k_dec_fused<F, T>, dim3(tiles_for(a.nunits)), 64u << wave_bits(T), tile_lds_bytes<F, T>(), s, &a,
+                  sizeof(a));
+}
+template <class F, int T>
+hipError_t enc_hi_t(const EncArgs& a, hipStream_t s) {
+    return launch(&k_enc_hi<F, T>, dim3(tiles_for(a.nunits), 1u << kLoBits), 64u << wave_bits(T),
+                  tile_lds_bytes<F, T>(), s, &a, sizeof(a));
+}
+template <class F, int T>
+hipError_t dec_hi_t(const DecArgs& a, hipStream_t s) {
+    return launch(&k_dec_hi<F, T>, dim3(tiles_for(a.nunits), 1u << kLoBits), 64u << wave_bits(T),
+                  tile_lds_bytes<F, T>(), s, &a, sizeof(a));
+}
+
+template <template <class, int> class Fn, class F, int TMIN, int TMAX, class A>
+hipError_t dispatch_T(unsigned T, const A& a, hipStream_t s) {
+    hipError_t e = hipErrorInvalidValue;
+    static_for<TMIN, TMAX + 1>([&](auto I) {
+        if (T == unsigned(decltype(I)::value)) e = Fn<F, decltype(I)::value>::run(a, s);
+    });
+    return e;
+}
+template <class F, int T>
+struct EncFusedFn { static hipError_t run(const EncArgs& a, hipStream_t s) { return enc_fused_t<F, T>(a, s); } };
+template <class F, int T>
+struct DecFusedFn { static hipError_t run(const DecArgs& a, hipStream_t s) { return dec_fused_t<F, T>(a, s); } };
+template <class F, int T>
+struct EncHiFn { static hipError_t run(const EncArgs& a, hipStream_t s) { return enc_hi_t<F, T>(a, s); } };
+template <class F, int T>
+struct DecHiFn { static hipError_t run(const DecArgs& a, hipStream_t s) { return dec_hi_t<F, T>(a, s); } };
+
+}  // namespace
+
+hipError_t launch_encode_fused(int ff16, unsigned T, const EncArgs& a, hipStream_t s) {
+    if (ff16) return dispatch_T<EncFusedFn, FF16, 1, 8>(T, a, s);
+    return dispatch_T<EncFusedFn, FF8, 1, 7>(T, a, s);
+}
+hipError_t launch_encode_lo(const EncArgs& a, hipStream_t s) {
+    const unsigned m = 1u << a.Tm;
+    return launch(&k_enc_lo<FF16>, dim3(tiles_for(a.nunits), m >> kLoBits, a.nchunks), 64u << wave_bits(kLoBits),
+                  tile_lds_bytes<FF16, kLoBits>(), s, &a, sizeof(a));
+}
+hipError_t launch_encode_hi(const EncArgs& a, hipStream_t s) {
+    return dispatch_T<EncHiFn, FF16, 1, 8>(a.Tm - kLoBits, a, s);
+}
+hipError_t launch_encode_fin(const EncArgs& a, hipStream_t s) {
+    const unsigned tiles = (a.R + (1u << kLoBits) - 1) >> kLoBits;
+    return launch(&k_enc_fin<FF16>, dim3(tiles_for(a.nunits), tiles), 64u << wave_bits(kLoBits),
+                  tile_lds_bytes<FF16, kLoBits>(), s, &a, sizeof(a));
+}
+hipError_t launch_decode_fused8(unsigned T, const DecArgs& a, hipStream_t s) {
+    return dispatch_T<DecFusedFn, FF8, 1, 8>(T, a, s);
+}
+hipError_t launch_decode_lo(const DecArgs& a, hipStream_t s) {
+    return launch(&k_dec_lo<FF16>, dim3(tiles_for(a.nunits), a.nlo), 64u << wave_bits(kLoBits),
+                  tile_lds_bytes<FF16, kLoBits>(), s, &a, sizeof(a));
+}
+hipError_t launch_decode_hi(const DecArgs& a, hipStream_t s) {
+    return dispatch_T<DecHiFn, FF16, 1, 8>(a.Tn - kLoBits, a, s);
+}
+hipError_t launch_decode_fin(const DecArgs& a, hipStream_t s) {
+    const unsigned n = 1u << a.Tn;
+    return launch(&k_dec_fin<FF16>, dim3(tiles_for(a.nunits), n >> kLoBits), 64u << wave_bits(kLoBits),
+                  tile_lds_bytes<FF16, kLoBits>(), s, &a, sizeof(a));
+}
+hipError_t launch_error_locator16(const uint32_t* erased, const uint32_t* walsh, uint32_t* tmp, uint32_t* el,
+                                  hipStream_t s) {
+    hipLaunchKernelGGL(k_el16_rows, dim3(256), dim3(64), 0, s, erased, tmp, el, 0);
+    hipLaunchKernelGGL(k_el16_cols, dim3(256), dim3(64), 0, s, tmp, walsh);
+    hipLaunchKernelGGL(k_el16_rows, dim3(256), dim3(64), 0, s, erased, tmp, el, 1);
+    return hipGetLastError();
+}
+hipError_t launch_xor_reduce(const XorArgs& a, hipStream_t s) {
+    const unsigned blocks = unsigned((a.ndwords / 4 + 255) / 256);
+    hipLaunchKernelGGL(k_xor_reduce, dim3(blocks), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace lamd

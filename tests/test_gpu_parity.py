@@ -1,0 +1,267 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle, the
+reference-generated golden fixtures, and size-independent properties at the
+BASELINE.json shapes.  Bit-exact everywhere (integer/byte work)."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib as ol
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def dev_tensor(a: np.ndarray):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def gpu_encode(leo, data: np.ndarray, r: int) -> np.ndarray:
+    out = leo.encode(dev_tensor(data), r)
+    torch.cuda.synchronize()
+    return out.cpu().numpy()
+
+
+def gpu_decode(leo, data, recovery, lost_o, lost_r):
+    res = leo.decode(dev_tensor(data), dev_tensor(recovery), lost_o, lost_r)
+    torch.cuda.synchronize()
+    return {i: v.cpu().numpy() for i, v in res.items()}
+
+
+# ---------------------------------------------------------------- encode --
+
+ENC_CASES = [
+    (2, 2, 64), (3, 2, 64), (4, 4, 128), (7, 5, 128), (16, 16, 64), (17, 16, 192), (32, 32, 256),
+    (33, 9, 64), (64, 64, 320), (100, 20, 64), (128, 128, 128), (130, 126, 64), (200, 55, 64), (250, 6, 64),
+    (5, 3, 64 * 17), (64, 64, 64 * 33),  # column tails that are not a whole tile
+    # FF16 single-tile encoders (m <= 256) and multi-pass ones (m > 256)
+    (129, 127, 64), (300, 37, 128), (1000, 200, 64), (700, 256, 128), (600, 300, 64), (5000, 3000, 64),
+    (2000, 1000, 128),
+]
+
+
+@pytest.mark.parametrize("k,r,b", ENC_CASES)
+def test_encode_matches_oracle(leo, k, r, b):
+    rng = np.random.default_rng(k * 7919 + r * 31 + b)
+    data = rng.integers(0, 256, (k, b), dtype=np.uint8)
+    expect = ol.oracle().encode(data, r)
+    got = gpu_encode(leo, data, r)
+    assert np.array_equal(got, expect)
+
+
+def _golden_small():
+    return np.load(os.path.join(GOLDEN, "golden_small.npz"))
+
+
+def _golden_keys(prefix):
+    with np.load(os.path.join(GOLDEN, "golden_small.npz")) as z:
+        return sorted(k for k in z.files if k.startswith(prefix))
+
+
+@pytest.mark.parametrize("key", _golden_keys("enc_"))
+def test_encode_matches_reference_golden(leo, key):
+    k, r, b = (int(x) for x in key.split("_")[1:])
+    with _golden_small() as z:
+        expect = z[key]
+    data = ol.pcg_bytes(2, 0, k, b)
+    got = gpu_encode(leo, data, r)
+    assert np.array_equal(got, expect)
+
+
+def test_encode_host_memory_matches_oracle(leo):
+    """Reference contract: caller-owned host buffers in and out (leopard.h:147-186)."""
+    for (k, r, b) in [(128, 128, 1024), (1000, 200, 256), (3, 2, 64)]:
+        rng = np.random.default_rng(k + r)
+        data = rng.integers(0, 256, (k, b), dtype=np.uint8)
+        wc = leo.leo_encode_work_count(k, r)
+        work = np.zeros((wc, b), dtype=np.uint8)
+        res = leo.leo_encode(b, k, r, wc, [data[i].ctypes.data for i in range(k)],
+                             [work[i].ctypes.data for i in range(wc)])
+        assert res == leo.LeopardResult.Success, leo.last_error()
+        assert np.array_equal(work[:r], ol.oracle().encode(data, r))
+
+
+# ---------------------------------------------------------------- decode --
+
+DEC_CASES = [  # (K, R, B, originals lost)
+    (2, 2, 64, 1), (3, 2, 64, 2), (7, 5, 128, 5), (16, 16, 64, 9), (100, 20, 64, 20), (128, 128, 128, 128),
+    (128, 128, 64, 1), (130, 126, 64, 100), (200, 55, 64, 55), (64, 64, 64 * 33, 40),
+    (129, 127, 64, 127), (300, 37, 128, 30), (1000, 200, 64, 200), (600, 300, 64, 299), (5000, 3000, 64, 3000),
+]
+
+
+@pytest.mark.parametrize("k,r,b,loss", DEC_CASES)
+def test_decode_roundtrip_and_oracle(leo, k, r, b, loss):
+    rng = np.random.default_rng(k * 13 + r + loss)
+    data = rng.integers(0, 256, (k, b), dtype=np.uint8)
+    rec = ol.oracle().encode(data, r)
+    lost_o = sorted(rng.choice(k, loss, replace=False).tolist())
+    lost_r = sorted(rng.choice(r, r - loss, replace=False).tolist())
+    got = gpu_decode(leo, data, rec, lost_o, lost_r)
+    for i in lost_o:
+        assert np.array_equal(got[i], data[i]), i
+    # non-codeword input: the exact decoder map must equal the oracle's
+    junk = rng.integers(0, 256, (r, b), dtype=np.uint8)
+    expect = ol.oracle().decode(data, junk, lost_o, lost_r)
+    got = gpu_decode(leo, data, junk, lost_o, lost_r)
+    for i in lost_o:
+        assert np.array_equal(got[i], expect[i]), i
+
+
+@pytest.mark.parametrize("key", _golden_keys("decout_"))
+def test_decode_matches_reference_golden(leo, key):
+    k, r, b, loss = (int(x) for x in key.split("_")[1:])
+    tag = "_".join(key.split("_")[1:])
+    with _golden_small() as z:
+        lo = z["declo_" + tag].tolist()
+        lr = z["declr_" + tag].tolist()
+        expect = z[key]
+    data = ol.pcg_bytes(2, 1, k, b)
+    rec = ol.pcg_bytes(2, 2, r, b)
+    got = gpu_decode(leo, data, rec, lo, lr)
+    for j, i in enumerate(lo):
+        assert np.array_equal(got[i], expect[j]), i
+
+
+def test_decode_benchmark_loss_pattern(leo):
+    """tests/benchmark.cpp:440-467 loss pattern with its self-checking packets."""
+    k, r, b = 1000, 200, 640
+    data = ol.pcg_bytes(2, 0, k, b)
+    rec = gpu_encode(leo, data, r)
+    lo, lr = ol.benchmark_losses(k, r, r, seed=2, trial=0, data_bytes=k * b)
+    got = gpu_decode(leo, data, rec, lo, lr)
+    for i in lo:
+        assert np.array_equal(got[i], data[i])
+
+
+def test_decode_host_memory(leo):
+    k, r, b = 128, 128, 512
+    rng = np.random.default_rng(5)
+    data = rng.integers(0, 256, (k, b), dtype=np.uint8)
+    rec = ol.oracle().encode(data, r)
+    lost = list(range(0, k, 2))
+    lost_r = list(range(len(lost), r))
+    wc = leo.leo_decode_work_count(k, r)
+    work = np.zeros((wc, b), dtype=np.uint8)
+    res = leo.leo_decode(b, k, r, wc, [None if i in lost else data[i].ctypes.data for i in range(k)],
+                         [None if i in lost_r else rec[i].ctypes.data for i in range(r)],
+                         [work[i].ctypes.data for i in range(wc)])
+    assert res == leo.LeopardResult.Success, leo.last_error()
+    for i in lost:
+        assert np.array_equal(work[i], data[i])
+
+
+# ------------------------------------------------------------ edge paths --
+
+def test_edge_paths(leo):
+    rng = np.random.default_rng(9)
+    # K == 1 (leopard.cpp:144-149, 279-283)
+    d = rng.integers(0, 256, (1, 128), dtype=np.uint8)
+    assert np.array_equal(gpu_encode(leo, d, 1), d)
+    # R == 1 parity (leopard.cpp:106-121, 214-231)
+    d = rng.integers(0, 256, (9, 192), dtype=np.uint8)
+    par = gpu_encode(leo, d, 1)
+    assert np.array_equal(par[0], np.bitwise_xor.reduce(d, axis=0))
+    got = gpu_decode(leo, d, par, [4], [])
+    assert np.array_equal(got[4], d[4])
+    # zero loss: every original copied to work (leopard.cpp:286-291)
+    d = rng.integers(0, 256, (20, 64), dtype=np.uint8)
+    rec = gpu_encode(leo, d, 5)
+    k, r = 20, 5
+    work = torch.zeros((leo.leo_decode_work_count(k, r), 64), dtype=torch.uint8, device="cuda")
+    dt, rt = dev_tensor(d), dev_tensor(rec)
+    res = leo.leo_decode(64, k, r, work.shape[0], [dt[i].data_ptr() for i in range(k)],
+                         [rt[i].data_ptr() for i in range(r)], [work[i].data_ptr() for i in range(work.shape[0])])
+    assert res == leo.LeopardResult.Success
+    assert np.array_equal(work[:k].cpu().numpy(), d)
+
+
+def test_error_codes(leo):
+    R = leo.LeopardResult
+    t = torch.zeros((8, 64), dtype=torch.uint8, device="cuda")
+    p = [t[i].data_ptr() for i in range(8)]
+    assert leo.leo_encode(63, 4, 2, 4, p[:4], p[4:]) == R.InvalidSize
+    assert leo.leo_encode(0, 4, 2, 4, p[:4], p[4:]) == R.InvalidSize
+    assert leo.leo_encode(64, 4, 5, 4, p[:4], p[4:]) == R.InvalidCounts
+    assert leo.leo_encode(64, 4, 0, 4, p[:4], p[4:]) == R.InvalidCounts
+    assert leo.leo_encode(64, 4, 2, 3, p[:4], p[4:]) == R.InvalidCounts
+    assert leo.leo_encode(64, 4, 2, 4, None, p[4:]) == R.InvalidInput
+    assert leo.leo_decode(64, 4, 2, 8, [None, None, None, p[3]], [p[4], p[5]], p) == R.NeedMoreData
+    assert leo.leo_decode(64, 4, 2, 7, [None, p[1], p[2], p[3]], [p[4], p[5]], p) == R.InvalidCounts
+    # n = NextPow2(NextPow2(R) + K) > 65536
+    assert leo.leo_encode_work_count(60000, 10000) == 32768
+    big = [p[0]] * 60000
+    assert leo.leo_encode(64, 60000, 10000, 32768, big, [p[1]] * 32768) == R.TooMuchData
+
+
+def test_slice_api_matches_whole(leo):
+    """Column sharding primitive: encoding byte ranges separately == whole."""
+    k, r, b = 100, 30, 64 * 40
+    rng = np.random.default_rng(11)
+    data = rng.integers(0, 256, (k, b), dtype=np.uint8)
+    expect = ol.oracle().encode(data, r)
+    dt = dev_tensor(data)
+    wc = leo.leo_encode_work_count(k, r)
+    work = torch.zeros((wc, b), dtype=torch.uint8, device="cuda")
+    for lo in range(0, b, 64 * 10):
+        res = leo.leo_amd_encode_slice(b, lo, 64 * 10, k, r, wc, [dt[i].data_ptr() for i in range(k)],
+                                       [work[i].data_ptr() for i in range(wc)])
+        assert res == leo.LeopardResult.Success
+    torch.cuda.synchronize()
+    assert np.array_equal(work[:r].cpu().numpy(), expect)
+
+
+def test_scattered_pointer_tables(leo):
+    """Non-slab piece arrays exercise the uploaded pointer-table path."""
+    k, r, b = 50, 20, 256
+    rng = np.random.default_rng(3)
+    data = rng.integers(0, 256, (k, b), dtype=np.uint8)
+    perm = rng.permutation(k)
+    store = dev_tensor(data[perm])  # piece i lives at row inv[i]
+    inv = np.argsort(perm)
+    wc = leo.leo_encode_work_count(k, r)
+    work = torch.zeros((wc, b), dtype=torch.uint8, device="cuda")
+    wperm = rng.permutation(wc)
+    res = leo.leo_encode(b, k, r, wc, [store[int(inv[i])].data_ptr() for i in range(k)],
+                         [work[int(wperm[i])].data_ptr() for i in range(wc)])
+    assert res == leo.LeopardResult.Success
+    torch.cuda.synchronize()
+    got = work.cpu().numpy()[wperm[:r]]
+    assert np.array_equal(got, ol.oracle().encode(data, r))
+
+
+# ----------------------------------------------- BASELINE shapes (full size) --
+
+def _digests():
+    path = os.path.join(GOLDEN, "golden_digests.json")
+    if not os.path.exists(path):
+        return {}
+    with open(path) as f:
+        return json.load(f).get("hash_digests", {})
+
+
+BIG = [(128, 128, 65536), (128, 128, 64000), (1000, 200, 65536), (1000, 200, 64000), (32768, 32768, 65536)]
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("k,r,b", BIG)
+def test_baseline_shapes_digest_and_roundtrip(leo, k, r, b):
+    key = f"{k}_{r}_{b}"
+    dig = _digests().get(key)
+    data = ol.hash_bytes_torch(7, k, b, "cuda")
+    rec = leo.encode(data, r)
+    torch.cuda.synchronize()
+    if dig is not None:
+        h = hashlib.sha256(rec.contiguous().cpu().numpy().tobytes()).hexdigest()
+        assert h == dig, "recovery bytes differ from the reference library's"
+    # worst case of the BASELINE configs: lose min(R, K) originals, benchmark pattern
+    lo, lr = ol.benchmark_losses(k, r, r, seed=2, trial=0)
+    got = leo.decode(data, rec, lo, lr)
+    torch.cuda.synchronize()
+    idx = torch.tensor(lo, device="cuda")
+    stacked = torch.stack([got[i] for i in lo])
+    assert torch.equal(stacked, data.index_select(0, idx))

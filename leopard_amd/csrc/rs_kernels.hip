@@ -175,28 +175,30 @@ __global__ void __launch_bounds__(64 << wave_bits(kLoBits)) k_enc_fin(EncArgs a)
 LDEV bool bit_set(const uint32_t* bits, unsigned p) { return (cload(bits + (p >> 5)) >> (p & 31)) & 1u; }
 
 // Erasure bitmap over codeword positions (bit p <=> error_locations[p] = 1,
-// LeopardFF8.cpp:1825-1840): FF8 passes it by value, FF16 in device memory.
-struct Erased8 {
-    uint32_t w[8];
-    LDEV bool get(unsigned p) const {
-        const unsigned i = p >> 5;
-        uint32_t v = w[0];
-#pragma unroll
-        for (unsigned k = 1; k < 8; ++k) v = i == k ? w[k] : v;
-        return (v >> (p & 31)) & 1u;
-    }
-};
+// LeopardFF8.cpp:1825-1840).  FF16 keeps it in device memory.
 struct ErasedDev {
     const uint32_t* bits;
     LDEV bool get(unsigned p) const { return bit_set(bits, p); }
 };
 
-// FF8 error locator inside the kernel: each wave evaluates all 256 entries,
-// lane holding positions lane + 64 j (LeopardFF8.cpp:1848-1853).  Fully reduced
-// mod 255 (congruent to the reference's partially reduced values; the
-// multiply tables treat 0 and 255 identically).
-struct El8 {
-    unsigned e[4];
+// Wave-uniform read of the value lane (p & 63) holds in register (p >> 6) of a
+// 4-register per-lane spread (positions lane + 64 j).  Only static register
+// indices and readlane: nothing is spilled to private memory.
+LDEV unsigned spread_at(const unsigned (&v)[4], unsigned p) {
+    const unsigned l = p & 63, j = p >> 6;
+    const unsigned a = __builtin_amdgcn_readlane(v[0], l), b = __builtin_amdgcn_readlane(v[1], l);
+    const unsigned c = __builtin_amdgcn_readlane(v[2], l), d = __builtin_amdgcn_readlane(v[3], l);
+    return j == 0 ? a : j == 1 ? b : j == 2 ? c : d;
+}
+
+// FF8 decoder state computed inside the kernel by every wave: erasure flags
+// and the error locator (LeopardFF8.cpp:1848-1853) for all 256 positions,
+// lane holding positions lane + 64 j.  Fully reduced mod 255 (congruent to
+// the reference's partially reduced values; the multiply tables treat 0 and
+// 255 identically).
+struct Dec8 {
+    unsigned e[4];  // error locator logs
+    unsigned f[4];  // erasure flags
     LDEV static unsigned addm(unsigned a, unsigned b) { unsigned s = a + b; return s >= 255u ? s - 255u : s; }
     LDEV static unsigned subm(unsigned a, unsigned b) { unsigned s = a + 255u - b; return s >= 255u ? s - 255u : s; }
     LDEV void fwht(unsigned lane) {
@@ -213,19 +215,20 @@ struct El8 {
         e[0] = addm(a0, a2); e[2] = subm(a0, a2);
         e[1] = addm(a1, a3); e[3] = subm(a1, a3);
     }
-    LDEV void compute(const Erased8& er, const uint32_t* __restrict__ walsh, unsigned lane) {
+    LDEV void compute(const uint32_t (&words)[8], const uint32_t* __restrict__ walsh, unsigned lane) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) e[j] = er.get(lane + 64 * j);
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t word = (lane & 32) ? words[2 * j + 1] : words[2 * j];
+            f[j] = (word >> (lane & 31)) & 1u;
+            e[j] = f[j];
+        }
         fwht(lane);
 #pragma unroll
         for (int j = 0; j < 4; ++j) e[j] = (e[j] * walsh[lane + 64 * j]) % 255u;
         fwht(lane);
     }
-    LDEV unsigned at(unsigned p) const {  // p wave-uniform
-        const unsigned j = p >> 6;
-        const unsigned v = j == 0 ? e[0] : j == 1 ? e[1] : j == 2 ? e[2] : e[3];
-        return __builtin_amdgcn_readlane(v, p & 63);
-    }
+    LDEV unsigned at(unsigned p) const { return spread_at(e, p); }
+    LDEV bool get(unsigned p) const { return spread_at(f, p) != 0; }
 };
 struct ElDev {
     const uint32_t* el;
@@ -274,11 +277,10 @@ __global__ void __launch_bounds__(64 << wave_bits(T)) k_dec_fused(DecArgs a) {
     const bool live = q0 < a.nunits;
     const uint64_t ql = live ? q0 : a.nunits - C;  // dead lanes re-read a valid unit: loads stay unpredicated
     const PieceSpace ps{0, 0, 0};
-    Erased8 erased;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) erased.w[k] = a.erased8[k];
-    El8 el;
-    el.compute(erased, a.walsh, lane);
+    Dec8 st;
+    st.compute(a.erased8, a.walsh, lane);
+    const Dec8& erased = st;
+    const Dec8& el = st;
 
     typename TL::Reg v, z;
 #pragma unroll

@@ -28,7 +28,7 @@ import os
 from typing import Optional, Sequence
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libleopard_amd.so")
+LIB_PATH = os.environ.get("LEOPARD_AMD_LIB") or os.path.join(_HERE, "lib", "libleopard_amd.so")
 LEO_VERSION = 2
 
 __all__ = [

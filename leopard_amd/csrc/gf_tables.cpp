@@ -140,4 +140,19 @@ void build_perm_tables16(const GaloisField& f, std::vector<uint32_t>& out) {
     }
 }
 
+void build_skew_tables(const GaloisField& f, const std::vector<uint32_t>& perm_tables, unsigned tab_dwords,
+                       unsigned flag_dw, std::vector<uint32_t>& out) {
+    out.assign(size_t(f.order()) * tab_dwords, 0);
+    for (unsigned i = 0; i < f.modulus(); ++i) {
+        uint32_t* e = &out[size_t(i) * tab_dwords];
+        const unsigned lm = f.skew[i];
+        if (lm == f.modulus()) {
+            e[flag_dw] = 1;  // zero skew: XOR only
+            continue;
+        }
+        const uint32_t* t = &perm_tables[size_t(lm) * tab_dwords];
+        for (unsigned d = 0; d < flag_dw; ++d) e[d] = t[d];
+    }
+}
+
 }  // namespace lamd

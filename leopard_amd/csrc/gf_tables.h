@@ -68,4 +68,14 @@ constexpr unsigned kTab16Dwords = 24;
 void build_perm_tables8(const GaloisField& f, std::vector<uint32_t>& out);
 void build_perm_tables16(const GaloisField& f, std::vector<uint32_t>& out);
 
+// Butterfly tables indexed by FFT-skew position i (not by log value): entry i
+// holds the multiply table of skew[i] and, in dword kSkewFlagDw, 1 when skew[i]
+// is the zero element (the butterfly then only XORs, LeopardFF8.cpp:690-708).
+// Kernels fetch entry (skew offset + group index) with one scalar load, with no
+// dependent skew -> log -> table chain.  order entries (the last is padding).
+constexpr unsigned kSkewFlagDw8 = 5;
+constexpr unsigned kSkewFlagDw16 = 20;
+void build_skew_tables(const GaloisField& f, const std::vector<uint32_t>& perm_tables, unsigned tab_dwords,
+                       unsigned flag_dw, std::vector<uint32_t>& out);
+
 }  // namespace lamd

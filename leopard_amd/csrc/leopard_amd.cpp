@@ -53,8 +53,8 @@ void set_error(const char* what, hipError_t e) {
 struct DeviceTables {
     uint32_t* tab8 = nullptr;   // (256 + 1) x 8 dwords
     uint32_t* tab16 = nullptr;  // (65536 + 1) x 24 dwords
-    uint32_t* skew8 = nullptr;  // 255 (+1 pad) entries
-    uint32_t* skew16 = nullptr;
+    uint32_t* sktab8 = nullptr;   // skew-indexed butterfly tables, 256 x 8 dwords
+    uint32_t* sktab16 = nullptr;  // 65536 x 24 dwords
     uint32_t* walsh8 = nullptr;
     uint32_t* walsh16 = nullptr;
     uint8_t* zeros = nullptr;   // zero page
@@ -65,7 +65,7 @@ std::mutex g_mu;
 bool g_initialized = false;
 int g_device_count = 0;
 std::vector<DeviceTables> g_dev;
-std::vector<uint32_t> g_h_tab8, g_h_tab16, g_h_skew8, g_h_skew16, g_h_walsh8, g_h_walsh16;
+std::vector<uint32_t> g_h_tab8, g_h_tab16, g_h_sktab8, g_h_sktab16, g_h_walsh8, g_h_walsh16;
 
 template <class T>
 hipError_t upload(T** dst, const std::vector<T>& src) {
@@ -84,8 +84,8 @@ LeopardResult ensure_device(int dev, DeviceTables** out) {
     if (!d.ready) {
         HIP_OK(upload(&d.tab8, g_h_tab8), "upload FF8 tables");
         HIP_OK(upload(&d.tab16, g_h_tab16), "upload FF16 tables");
-        HIP_OK(upload(&d.skew8, g_h_skew8), "upload FF8 skew");
-        HIP_OK(upload(&d.skew16, g_h_skew16), "upload FF16 skew");
+        HIP_OK(upload(&d.sktab8, g_h_sktab8), "upload FF8 skew tables");
+        HIP_OK(upload(&d.sktab16, g_h_sktab16), "upload FF16 skew tables");
         HIP_OK(upload(&d.walsh8, g_h_walsh8), "upload FF8 LogWalsh");
         HIP_OK(upload(&d.walsh16, g_h_walsh16), "upload FF16 LogWalsh");
         HIP_OK(hipMalloc(reinterpret_cast<void**>(&d.zeros), 4096), "zero page");
@@ -282,7 +282,7 @@ LeopardResult encode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
     MapBuilder mb;
     mb.build(a.in, orig, K, off);
     mb.build(a.out, work, R, off);
-    a.skew = ff16 ? c.t->skew16 : c.t->skew8;
+    a.sktab = ff16 ? c.t->sktab16 : c.t->sktab8;
     a.tabs = ff16 ? c.t->tab16 : c.t->tab8;
     a.zeros = c.t->zeros;
     a.K = K;
@@ -361,7 +361,7 @@ LeopardResult decode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
     mb.build(a.orig, orig, K, off);
     mb.build(a.rec, rec, R, off);
     mb.build(a.out, work, K, off);
-    a.skew = ff16 ? c.t->skew16 : c.t->skew8;
+    a.sktab = ff16 ? c.t->sktab16 : c.t->sktab8;
     a.tabs = ff16 ? c.t->tab16 : c.t->tab8;
     a.zeros = c.t->zeros;
     a.walsh = ff16 ? c.t->walsh16 : c.t->walsh8;
@@ -391,25 +391,42 @@ LeopardResult decode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
         return Leopard_Success;
     }
 
-    // FF16: erasure bitmap (full 65536 positions) + error locator on the device
+    // FF16: erasure bitmap (full 65536 positions) + error locator on the device,
+    // plus occupancy pyramids for pruning (received data / lost originals).
     const size_t bitmap_words = 65536 / 32;
+    std::vector<uint32_t> pyr_present(kPyrWords, 0), pyr_needed(kPyrWords, 0);
+    {
+        auto mark = [](std::vector<uint32_t>& pyr, unsigned p) {
+            for (unsigned L = 0; L <= 16; ++L) {
+                const unsigned j = p >> L;
+                pyr[pyr_offset(L) + (j >> 5)] |= 1u << (j & 31);
+            }
+        };
+        for (unsigned i = 0; i < R; ++i)
+            if (rec[i]) mark(pyr_present, i);
+        for (unsigned i = 0; i < K; ++i) mark(orig[i] ? pyr_present : pyr_needed, m + i);
+    }
     const uint64_t slab_pieces = 3ull * n;
     const uint64_t slice = mall_slice(bytes, slab_pieces);
     const size_t table_bytes = (mb.bytes() + 255) / 256 * 256;
     const size_t off_bitmap = table_bytes;
     const size_t off_tmp = off_bitmap + bitmap_words * 4;
     const size_t off_el = off_tmp + 65536 * 4;
-    const size_t off_slab = off_el + 65536 * 4;
+    const size_t off_pyr = off_el + 65536 * 4;
+    const size_t off_slab = off_pyr + 2 * kPyrWords * 4 + 256;
     LeopardResult r = c.ws->reserve_device(off_slab + slab_pieces * slice);
     if (r != Leopard_Success) return r;
     // stage tables + bitmap together
     std::vector<uint32_t> bitmap(bitmap_words, 0);
     std::copy(erased.begin(), erased.end(), bitmap.begin());
-    const size_t stage_bytes = table_bytes + bitmap_words * 4;
+    // staged image mirrors the device layout from offset 0 up to the slabs
+    const size_t stage_bytes = off_slab;
     r = c.ws->reserve_stage(stage_bytes);
     if (r != Leopard_Success) return r;
     if (!mb.staged.empty()) std::memcpy(c.ws->hstage, mb.staged.data(), mb.bytes());
     std::memcpy(c.ws->hstage + off_bitmap, bitmap.data(), bitmap_words * 4);
+    std::memcpy(c.ws->hstage + off_pyr, pyr_present.data(), kPyrWords * 4);
+    std::memcpy(c.ws->hstage + off_pyr + kPyrWords * 4, pyr_needed.data(), kPyrWords * 4);
     HIP_OK(hipMemcpyAsync(c.ws->dbuf, c.ws->hstage, stage_bytes, hipMemcpyHostToDevice, c.s), "upload decode state");
     HIP_OK(hipEventRecord(c.ws->stage_done, c.s), "record staging");
     c.ws->stage_pending = true;
@@ -421,6 +438,8 @@ LeopardResult decode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
     HIP_OK(launch_error_locator16(d_bitmap, c.t->walsh16, d_tmp, d_el, c.s), "error locator");
     a.el = d_el;
     a.erased_dev = d_bitmap;
+    a.present_pyr = reinterpret_cast<uint32_t*>(c.ws->dbuf + off_pyr);
+    a.needed_pyr = a.present_pyr + kPyrWords;
     a.nlo = (m + K + (1u << kLoBits) - 1) >> kLoBits;
 
     uint8_t* A = c.ws->dbuf + off_slab;
@@ -716,10 +735,8 @@ LEO_EXPORT int leo_init_(int version) {
     const GaloisField& f16 = field16();
     build_perm_tables8(f8, g_h_tab8);
     build_perm_tables16(f16, g_h_tab16);
-    g_h_skew8.assign(f8.skew.begin(), f8.skew.end());
-    g_h_skew8.push_back(0);
-    g_h_skew16.assign(f16.skew.begin(), f16.skew.end());
-    g_h_skew16.push_back(0);
+    build_skew_tables(f8, g_h_tab8, kTab8Dwords, kSkewFlagDw8, g_h_sktab8);
+    build_skew_tables(f16, g_h_tab16, kTab16Dwords, kSkewFlagDw16, g_h_sktab16);
     g_h_walsh8.assign(f8.log_walsh.begin(), f8.log_walsh.end());
     g_h_walsh16.assign(f16.log_walsh.begin(), f16.log_walsh.end());
     g_dev.assign(count, DeviceTables{});

@@ -11,13 +11,19 @@ namespace lamd {
 // workgroup tile; the remaining high bits form the second tile).
 constexpr unsigned kLoBits = 8;
 
+// Occupancy pyramid over 65536 codeword positions: level L (0..16) has one bit
+// per aligned block of 2^L positions, set when any position in the block is set.
+// Level L starts at word pyr_offset(L).
+__host__ __device__ inline unsigned pyr_offset(unsigned L) { return L <= 12 ? 4096u - (4096u >> L) : 4095u + (L - 12); }
+constexpr unsigned kPyrWords = 4100;
+
 struct EncArgs {
     PieceMap in;        // originals (K)
     PieceMap out;       // recovery destinations (R)
     PieceMap slab_in;   // multi-pass intermediate read
     PieceMap slab_out;  // multi-pass intermediate write
-    const uint32_t* skew;
-    const uint32_t* tabs;   // multiply tables; entry kModulus+1 is all zero
+    const uint32_t* sktab;  // butterfly tables indexed by skew position (gf_tables.h)
+    const uint32_t* tabs;   // multiply tables by log value; entry kModulus+1 is all zero
     const uint8_t* zeros;   // >= 256 zero bytes
     unsigned K, R, Tm, nchunks;
     uint64_t nunits;  // column units in this launch
@@ -26,10 +32,12 @@ struct EncArgs {
 struct DecArgs {
     PieceMap orig, rec, out;
     PieceMap a_in, b_in, a_out, b_out;  // multi-pass intermediates
-    const uint32_t* skew;
+    const uint32_t* sktab;
     const uint32_t* tabs;
     const uint8_t* zeros;
-    const uint32_t* walsh;       // FF8: LogWalsh for the in-kernel error locator
+    const uint32_t* walsh;
+    const uint32_t* present_pyr;  // FF16: "any received data" pyramid over positions
+    const uint32_t* needed_pyr;   // FF16: "any lost original" pyramid over positions       // FF8: LogWalsh for the in-kernel error locator
     const uint32_t* el;          // FF16: precomputed error locator logs
     const uint32_t* erased_dev;  // FF16: erasure bitmap over positions [0, n)
     uint32_t erased8[8];         // FF8: erasure bitmap by value

@@ -25,6 +25,14 @@
 
 #define LDEV __device__ __forceinline__
 
+// Ablation switches for performance experiments only (tools/ablate.sh builds
+// separate libraries with them; the shipped library has LAMD_ABLATE == 0):
+// 1 = no butterfly arithmetic, 2 = no LDS transposes, 4 = no piece loads,
+// 8 = no piece stores.
+#ifndef LAMD_ABLATE
+#define LAMD_ABLATE 0
+#endif
+
 namespace lamd {
 
 LDEV uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) { return __builtin_amdgcn_perm(hi, lo, sel); }
@@ -61,15 +69,21 @@ __host__ __device__ __forceinline__ void static_for(Fn&& fn) {
 
 struct FF8 {
     static constexpr int kBits = 8;
+    static constexpr unsigned kOrder = 256;
     static constexpr int kDw = 1;  // dwords per unit
     static constexpr unsigned kModulus = 255;
     static constexpr unsigned kTabDw = 8;
+    static constexpr unsigned kFlagDw = 5;  // skew-indexed tables: 1 = zero skew
     struct Tab {
         uint32_t a0, a1, b0, b1, c0;
     };
-    LDEV static Tab tab(const uint32_t* tabs, unsigned log_m) {
-        const uint32_t* p = tabs + log_m * kTabDw;
+    LDEV static Tab tab_at(const uint32_t* p) {
         return Tab{cload(p), cload(p + 1), cload(p + 2), cload(p + 3), cload(p + 4)};
+    }
+    LDEV static Tab tab(const uint32_t* tabs, unsigned log_m) { return tab_at(tabs + log_m * kTabDw); }
+    LDEV static Tab tab_lds(const uint32_t* p) {
+        const uint4 v = *reinterpret_cast<const uint4*>(p);
+        return Tab{v.x, v.y, v.z, v.w, p[4]};
     }
     LDEV static uint32_t prod(uint32_t y, const Tab& t) {
         const uint32_t s0 = y & 0x07070707u;
@@ -89,17 +103,31 @@ struct FF8 {
 
 struct FF16 {
     static constexpr int kBits = 16;
+    static constexpr unsigned kOrder = 65536;
     static constexpr int kDw = 2;  // [0] low bytes of 4 elements, [1] their high bytes
     static constexpr unsigned kModulus = 65535;
     static constexpr unsigned kTabDw = 24;
+    static constexpr unsigned kFlagDw = 20;
     struct Tab {
         uint32_t t[20];
     };
-    LDEV static Tab tab(const uint32_t* tabs, unsigned log_m) {
-        const uint32_t* p = tabs + log_m * kTabDw;
+    LDEV static Tab tab_at(const uint32_t* p) {
         Tab r;
 #pragma unroll
         for (int i = 0; i < 20; ++i) r.t[i] = cload(p + i);
+        return r;
+    }
+    LDEV static Tab tab(const uint32_t* tabs, unsigned log_m) { return tab_at(tabs + log_m * kTabDw); }
+    LDEV static Tab tab_lds(const uint32_t* p) {
+        Tab r;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            const uint4 v = reinterpret_cast<const uint4*>(p)[i];
+            r.t[4 * i] = v.x;
+            r.t[4 * i + 1] = v.y;
+            r.t[4 * i + 2] = v.z;
+            r.t[4 * i + 3] = v.w;
+        }
         return r;
     }
     // (pl, ph) = (lo, hi) * c, see gf_tables.h for the table layout
@@ -174,6 +202,10 @@ LDEV void vstore(uint8_t* dst, const uint32_t* src) {
 // x[2u] = low-byte dword, x[2u+1] = high-byte dword of unit u.
 template <class F, int C>
 LDEV void load_units(uint32_t* x, const uint8_t* piece, uint64_t q0) {
+    if constexpr ((LAMD_ABLATE & 4) != 0) {
+        for (int k = 0; k < C * F::kDw; ++k) x[k] = uint32_t(q0) * 2654435761u + uint32_t(uintptr_t(piece));
+        return;
+    }
     if constexpr (F::kDw == 1) {
         vload<C>(x, piece + q0 * 4);
     } else {
@@ -187,6 +219,12 @@ LDEV void load_units(uint32_t* x, const uint8_t* piece, uint64_t q0) {
 }
 template <class F, int C>
 LDEV void store_units(uint8_t* piece, uint64_t q0, const uint32_t* x) {
+    if constexpr ((LAMD_ABLATE & 8) != 0) {
+        uint32_t acc = 0;
+        for (int k = 0; k < C * F::kDw; ++k) acc ^= x[k];
+        if (acc == 0x9E3779B9u && q0 == 0x7FFFFFFFull) *reinterpret_cast<uint32_t*>(piece) = acc;  // keep x live
+        return;
+    }
     if constexpr (F::kDw == 1) {
         vstore<C>(piece + q0 * 4, x);
     } else {
@@ -201,6 +239,48 @@ LDEV void store_units(uint8_t* piece, uint64_t q0, const uint32_t* x) {
 
 // ------------------------------------------------------------- tile engine --
 
+// Butterfly tables of one transform stage.  A stage with skew base `off`
+// needs the skew-indexed entries off + cidx for the group indices cidx its tile
+// produces.
+//
+// LdsWindow (FF8: 5-dword tables) stages them in LDS: slot (cidx - base) >>
+// shift holds entry off + cidx.  Whole-transform tiles: base 0, shift 0; tiles
+// of the low 8 bits (other bits fixed to y): base y << 8; tiles of the high
+// bits: cidx is a multiple of 256, shift 8.  Tables land in VGPRs (ds_read),
+// so v_perm needs no SGPR->VGPR copies.
+//
+// GlobalWindow (FF16: 20-dword tables) reads entries straight from the global
+// skew-indexed array through the scalar cache (20 SGPRs per table).
+template <class F>
+struct LdsWindow {
+    uint32_t* lds;
+    unsigned base, shift, count;
+    LDEV typename F::Tab table(unsigned cidx) const {
+        return F::tab_lds(lds + ((cidx - base) >> shift) * F::kTabDw);
+    }
+    // Cooperative refill by the whole workgroup (barriers on both sides).
+    LDEV void fill(const uint32_t* sktab, int off) {
+        __syncthreads();
+        const unsigned total = count * F::kTabDw;
+        for (unsigned i = threadIdx.x; i < total; i += blockDim.x) {
+            const unsigned slot = i / F::kTabDw, d = i - slot * F::kTabDw;
+            const long g = long(off) + long(base) + (long(slot) << shift);
+            lds[i] = (g >= 0 && g < long(F::kOrder)) ? sktab[size_t(g) * F::kTabDw + d] : 0u;
+        }
+        __syncthreads();
+    }
+    static constexpr size_t lds_dwords(unsigned count) { return size_t(count) * F::kTabDw; }
+};
+template <class F>
+struct GlobalWindow {
+    const uint32_t* sk = nullptr;
+    LDEV typename F::Tab table(unsigned cidx) const { return F::tab_at(sk + size_t(cidx) * F::kTabDw); }
+    LDEV void fill(const uint32_t* sktab, int off) { sk = sktab + ptrdiff_t(off) * ptrdiff_t(F::kTabDw); }
+    static constexpr size_t lds_dwords(unsigned) { return 0; }
+};
+template <class F>
+using WindowFor = typename std::conditional<F::kDw == 1, LdsWindow<F>, GlobalWindow<F>>::type;
+
 // Global piece index of tile piece tp:  lo_fixed | tp << l0 | hi_fixed.
 struct PieceSpace {
     unsigned lo_fixed, l0, hi_fixed;
@@ -212,18 +292,31 @@ struct PieceSpace {
 // form of LeopardFF8.cpp:1111-1114 / 1557-1560).
 LDEV unsigned skew_index(unsigned i, unsigned l) { return ((i >> l) | 1u) << l; }
 
-template <class F, int T, int H, int C>
+// A tile: 2^T pieces x (64*C) units.  Each lane holds NR = 2^R pieces in
+// registers; a "layout" k assigns tile bits [lo(k), lo(k) + R) to the register
+// index and the remaining T-R bits, in order, to the wave index (2^(T-R) waves).
+// Layouts k = 0 .. NL-1 step upward through the bits (the last one holds the
+// top R bits); a butterfly layer on tile bit l runs in a layout holding bit l
+// in registers, and an LDS transpose moves the tile between adjacent layouts.
+template <class F, int T, int R, int C>
 struct Tile {
-    static_assert(T - H >= H, "high layout needs T-H >= H");
-    static constexpr int NR = 1 << (T - H);  // pieces per lane
+    static_assert(R >= 1 && R <= T, "register bits");
+    static constexpr int NR = 1 << R;         // pieces per lane
     static constexpr int U = C * F::kDw;      // dwords per piece per lane
-    static constexpr int NW = 1 << H;         // waves per workgroup
+    static constexpr int NW = 1 << (T - R);   // waves per workgroup
+    static constexpr int NL = (T + R - 1) / R;
+    static constexpr int kLast = NL - 1;
     using Reg = uint32_t[NR][U];
 
-    // tile piece held in register r by wave w.  Layout 0: register index =
-    // tile bits [0, T-H); layout 1: register index = tile bits [H, T).
-    LDEV static unsigned piece(int lay, int r, unsigned w) {
-        return lay == 0 ? (unsigned(r) | (w << (T - H))) : (w | (unsigned(r) << H));
+    static constexpr int lo(int k) { return k * R < T - R ? k * R : T - R; }
+    // IFFT layers done in layout k: [ifft_begin(k), lo(k) + R); FFT layers: [lo(k), fft_end(k))
+    static constexpr int ifft_begin(int k) { return k == 0 ? 0 : lo(k - 1) + R; }
+    static constexpr int fft_end(int k) { return k == NL - 1 ? T : lo(k + 1); }
+
+    // tile piece held in register r by wave w in layout k
+    LDEV static unsigned piece(int k, int r, unsigned w) {
+        const int b = lo(k);
+        return (w & ((1u << b) - 1)) | (unsigned(r) << b) | ((w >> b) << (b + R));
     }
 
     LDEV static void zero(Reg& x) {
@@ -248,112 +341,133 @@ struct Tile {
     // One butterfly layer on tile bit L (compile time) in layout LAY.
     //   IFFT (LeopardFF8.cpp:595-666):  y ^= x; x ^= y * skew   (skipped if skew is 0)
     //   FFT  (LeopardFF8.cpp:1319-1390): x ^= y * skew; y ^= x
-    template <bool kInverse, int LAY, int L>
-    LDEV static void layer(Reg& x, unsigned w, const PieceSpace& ps, const uint32_t* __restrict__ skew,
-                           const uint32_t* __restrict__ tabs) {
-        constexpr int rb = LAY == 0 ? L : L - H;
-        static_assert(rb >= 0 && rb < T - H, "layer not in this layout");
+    // win holds the stage's butterfly tables (skew base already applied).
+    template <bool kInverse, int LAY, int L, class Win>
+    LDEV static void layer(Reg& x, unsigned w, const PieceSpace& ps, const Win& win) {
+        if constexpr ((LAMD_ABLATE & 1) != 0) return;
+        constexpr int rb = L - lo(LAY);
+        static_assert(rb >= 0 && rb < R, "layer not in this layout");
         constexpr int half = 1 << rb;
         const unsigned gl = ps.l0 + L;
+        auto table = [&](int g) {
+            // A zero skew has an all-zero table: the multiply-add adds 0, which is
+            // the reference's XOR-only butterfly without a branch (branches around
+            // register-array updates cost whole-array copies at the merge).
+            return win.table(skew_index(ps.global(piece(LAY, g, w)), gl));
+        };
+        constexpr int NG = NR / (2 * half);  // groups (distinct skews) per lane in this layer
+        auto group = [&](int g, const typename F::Tab& t) {
 #pragma unroll
-        for (int g = 0; g < NR; g += 2 * half) {
-            const unsigned gp = ps.global(piece(LAY, g, w));
-            const unsigned lm = cload(skew + skew_index(gp, gl));
-            if (lm != F::kModulus) {
-                const typename F::Tab t = F::tab(tabs, lm);
+            for (int j = 0; j < half; ++j) {
 #pragma unroll
-                for (int j = 0; j < half; ++j) {
+                for (int u = 0; u < C; ++u) {
+                    uint32_t* a = &x[g + j][u * F::kDw];
+                    uint32_t* b = &x[g + j + half][u * F::kDw];
+                    if constexpr (kInverse) {
 #pragma unroll
-                    for (int u = 0; u < C; ++u) {
-                        uint32_t* a = &x[g + j][u * F::kDw];
-                        uint32_t* b = &x[g + j + half][u * F::kDw];
-                        if constexpr (kInverse) {
+                        for (int k = 0; k < F::kDw; ++k) b[k] ^= a[k];
+                        F::muladd(a, b, t);
+                    } else {
+                        F::muladd(a, b, t);
 #pragma unroll
-                            for (int k = 0; k < F::kDw; ++k) b[k] ^= a[k];
-                            F::muladd(a, b, t);
-                        } else {
-                            F::muladd(a, b, t);
-#pragma unroll
-                            for (int k = 0; k < F::kDw; ++k) b[k] ^= a[k];
-                        }
+                        for (int k = 0; k < F::kDw; ++k) b[k] ^= a[k];
                     }
                 }
-            } else {
-#pragma unroll
-                for (int j = 0; j < half; ++j)
-#pragma unroll
-                    for (int k = 0; k < U; ++k) x[g + j + half][k] ^= x[g + j][k];
             }
+        };
+        if constexpr (F::kDw == 1) {
+            // FF8 (5-dword tables): read every table of the layer, then let the
+            // scheduler interleave the layer's independent butterflies (ILP).
+            typename F::Tab tabs[NG];
+            static_for<0, NG>([&](auto GI) { tabs[GI.value] = table(GI.value * 2 * half); });
+            static_for<0, NG>([&](auto GI) { group(GI.value * 2 * half, tabs[GI.value]); });
+            __builtin_amdgcn_sched_barrier(0);  // keep the next layer's tables below this one
+        } else {
+            // FF16 (20-dword tables in SGPRs): software pipeline, two tables live.
+            typename F::Tab next = table(0);
+            static_for<0, NG>([&](auto GI) {
+                constexpr int g = decltype(GI)::value * 2 * half;
+                const typename F::Tab t = next;
+                if constexpr (g + 2 * half < NR) next = table(g + 2 * half);
+                __builtin_amdgcn_sched_barrier(0);
+                group(g, t);
+                __builtin_amdgcn_sched_barrier(0);
+            });
         }
     }
 
-    // Move the tile between layouts through LDS (lds: 2^T * 64 * U dwords).
-    template <int FROM>
+    // Move the tile from layout FROM to layout TO through LDS (2^T * 64 * U dwords).
+    template <int FROM, int TO>
     LDEV static void transpose(Reg& x, unsigned w, unsigned lane, uint32_t* lds) {
-        if constexpr (H > 0) {
-            __syncthreads();
+        if constexpr ((LAMD_ABLATE & 2) != 0) return;
+        __syncthreads();
 #pragma unroll
-            for (int r = 0; r < NR; ++r) {
-                uint32_t* p = lds + (size_t(piece(FROM, r, w)) * 64 + lane) * U;
+        for (int r = 0; r < NR; ++r) {
+            uint32_t* p = lds + (size_t(piece(FROM, r, w)) * 64 + lane) * U;
 #pragma unroll
-                for (int k = 0; k < U; ++k) p[k] = x[r][k];
-            }
-            __syncthreads();
+            for (int k = 0; k < U; ++k) p[k] = x[r][k];
+        }
+        __syncthreads();
 #pragma unroll
-            for (int r = 0; r < NR; ++r) {
-                const uint32_t* p = lds + (size_t(piece(1 - FROM, r, w)) * 64 + lane) * U;
+        for (int r = 0; r < NR; ++r) {
+            const uint32_t* p = lds + (size_t(piece(TO, r, w)) * 64 + lane) * U;
 #pragma unroll
-                for (int k = 0; k < U; ++k) x[r][k] = p[k];
-            }
+            for (int k = 0; k < U; ++k) x[r][k] = p[k];
         }
     }
 
-    // IFFT over all tile bits: starts in layout 0, ends in layout 1.
-    LDEV static void ifft(Reg& x, unsigned w, unsigned lane, uint32_t* lds, const PieceSpace& ps,
-                          const uint32_t* skew, const uint32_t* tabs) {
-        static_for<0, T - H>([&](auto L) { layer<true, 0, decltype(L)::value>(x, w, ps, skew, tabs); });
-        transpose<0>(x, w, lane, lds);
-        static_for<T - H, T>([&](auto L) { layer<true, 1, decltype(L)::value>(x, w, ps, skew, tabs); });
+    // IFFT over all tile bits: starts in layout 0, ends in layout kLast.
+    template <class Win>
+    LDEV static void ifft(Reg& x, unsigned w, unsigned lane, uint32_t* lds, const PieceSpace& ps, const Win& win) {
+        static_for<0, NL>([&](auto K) {
+            constexpr int k = decltype(K)::value;
+            static_for<ifft_begin(k), lo(k) + R>([&](auto L) { layer<true, k, decltype(L)::value>(x, w, ps, win); });
+            if constexpr (k + 1 < NL) transpose<k, k + 1>(x, w, lane, lds);
+        });
     }
 
-    // FFT over all tile bits: starts in layout 1, ends in layout 0.
-    LDEV static void fft(Reg& x, unsigned w, unsigned lane, uint32_t* lds, const PieceSpace& ps,
-                         const uint32_t* skew, const uint32_t* tabs) {
-        static_for<0, H>([&](auto I) { layer<false, 1, T - 1 - decltype(I)::value>(x, w, ps, skew, tabs); });
-        transpose<1>(x, w, lane, lds);
-        static_for<0, T - H>([&](auto I) { layer<false, 0, T - H - 1 - decltype(I)::value>(x, w, ps, skew, tabs); });
+    // FFT over all tile bits: starts in layout kLast, ends in layout 0.
+    template <class Win>
+    LDEV static void fft(Reg& x, unsigned w, unsigned lane, uint32_t* lds, const PieceSpace& ps, const Win& win) {
+        static_for<0, NL>([&](auto KI) {
+            constexpr int k = NL - 1 - decltype(KI)::value;
+            static_for<lo(k), fft_end(k)>([&](auto LI) {
+                constexpr int L = fft_end(k) - 1 - (decltype(LI)::value - lo(k));
+                layer<false, k, L>(x, w, ps, win);
+            });
+            if constexpr (k > 0) transpose<k, k - 1>(x, w, lane, lds);
+        });
     }
 
-    // d += sum over tile bits b with bit b of k clear of v[k | 2^b]   (layout 1).
+    // d += sum over tile bits b with bit b of k clear of v[k | 2^b]   (layout kLast,
+    // whose registers hold the top R bits and whose wave index is bits [0, T-R)).
     // This is the tile's share of Leopard's formal derivative; with d = v it is
     // the whole derivative of a transform that fits the tile (closed form of
     // the loop at LeopardFF8.cpp:1890-1899: every source is read before it is
     // modified, so out[k] = v[k] ^ XOR_{b: k_b = 0} v[k | 2^b]).
     LDEV static void derivative_add(Reg& d, const Reg& v, unsigned w, unsigned lane, uint32_t* lds) {
-        // register bits (tile bits H .. T-1)
 #pragma unroll
         for (int r = 0; r < NR; ++r)
 #pragma unroll
-            for (int b = 0; b < T - H; ++b)
+            for (int b = 0; b < R; ++b)
                 if (!(r & (1 << b)))
 #pragma unroll
                     for (int k = 0; k < U; ++k) d[r][k] ^= v[r | (1 << b)][k];
-        // wave bits (tile bits 0 .. H-1) through LDS
-        if constexpr (H > 0) {
+        if constexpr (T > R) {
             __syncthreads();
 #pragma unroll
             for (int r = 0; r < NR; ++r) {
-                uint32_t* p = lds + (size_t(piece(1, r, w)) * 64 + lane) * U;
+                uint32_t* p = lds + (size_t(piece(kLast, r, w)) * 64 + lane) * U;
 #pragma unroll
                 for (int k = 0; k < U; ++k) p[k] = v[r][k];
             }
             __syncthreads();
-            for (int b = 0; b < H; ++b) {
+            for (int b = 0; b < T - R; ++b) {
                 if (w & (1u << b)) continue;  // wave-uniform
                 const unsigned w2 = w | (1u << b);
 #pragma unroll
                 for (int r = 0; r < NR; ++r) {
-                    const uint32_t* p = lds + (size_t(piece(1, r, w2)) * 64 + lane) * U;
+                    const uint32_t* p = lds + (size_t(piece(kLast, r, w2)) * 64 + lane) * U;
 #pragma unroll
                     for (int k = 0; k < U; ++k) d[r][k] ^= p[k];
                 }

@@ -27,12 +27,27 @@ namespace {
 
 constexpr int C = kUnitsPerLane;
 
-constexpr int wave_bits(int T) { return T <= 4 ? 0 : T - 4; }
+// Register bits per lane for a tile of T bits: 8 pieces per lane when that
+// gives at most 16 waves (more waves per SIMD hide the butterfly chains'
+// latency), otherwise 16 pieces (T = 8: 16 waves of 16 pieces).
+constexpr int reg_bits(int T) { return T <= 3 ? T : (T - 3 <= 4 ? 3 : T - 4); }
+constexpr int wave_bits(int T) { return T - reg_bits(T); }
 
+// LDS carve-up: [tile transpose area][butterfly-table window][FF8 decoder: log tables]
 template <class F, int T>
-constexpr size_t tile_lds_bytes() {
-    return wave_bits(T) > 0 ? (size_t(1) << T) * 64 * C * F::kDw * 4 : 0;
+constexpr size_t tile_lds_dwords() {
+    return wave_bits(T) > 0 ? (size_t(1) << T) * 64 * C * F::kDw : 0;  // transposes
 }
+template <class F>
+constexpr size_t window_dwords(unsigned entries) {
+    return WindowFor<F>::lds_dwords(entries);
+}
+template <class F>
+LDEV WindowFor<F> make_window(uint32_t* lds, unsigned base, unsigned shift, unsigned count) {
+    if constexpr (F::kDw == 1) return LdsWindow<F>{lds, base, shift, count};
+    else return GlobalWindow<F>{};
+}
+constexpr size_t kLogTab8Dwords = 257 * FF8::kTabDw;
 
 LDEV uint64_t lane_units(unsigned lane) { return (uint64_t(blockIdx.x) * 64 + lane) * C; }
 
@@ -49,10 +64,10 @@ LDEV void load_or_zero(uint32_t* x, const PieceMap& pm, bool ok, unsigned i, con
 // ------------------------------------------------------------------ encode --
 
 template <class F, int T>
-__global__ void __launch_bounds__(64 << wave_bits(T)) k_enc_fused(EncArgs a) {
-    constexpr int H = wave_bits(T);
-    using TL = Tile<F, T, H, C>;
+__global__ void __launch_bounds__(64 << wave_bits(T), 4) k_enc_fused(EncArgs a) {
+    using TL = Tile<F, T, reg_bits(T), C>;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    WindowFor<F> win = make_window<F>(lds + tile_lds_dwords<F, T>(), 0, 0, 1u << T);
     const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const uint64_t q0 = lane_units(lane);
     const bool live = q0 < a.nunits;
@@ -68,11 +83,13 @@ __global__ void __launch_bounds__(64 << wave_bits(T)) k_enc_fused(EncArgs a) {
             const unsigned tp = TL::piece(0, r, w);
             load_or_zero<F>(x[r], a.in, tp < cnt, base + tp, a.zeros, ql);
         }
-        TL::ifft(x, w, lane, lds, ps, a.skew + (m - 1 + base), a.tabs);
+        win.fill(a.sktab, int(m - 1 + base));
+        TL::ifft(x, w, lane, lds, ps, win);
         if (c == 0) TL::copy(acc, x);
         else TL::xor_into(acc, x);
     }
-    TL::fft(acc, w, lane, lds, ps, a.skew - 1, a.tabs);
+    win.fill(a.sktab, -1);
+    TL::fft(acc, w, lane, lds, ps, win);
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) {
         const unsigned tp = TL::piece(0, r, w);
@@ -82,14 +99,15 @@ __global__ void __launch_bounds__(64 << wave_bits(T)) k_enc_fused(EncArgs a) {
 
 // pass 1: IFFT over the low kLoBits of chunk blockIdx.z -> slab_out[c*m + g]
 template <class F>
-__global__ void __launch_bounds__(64 << wave_bits(kLoBits)) k_enc_lo(EncArgs a) {
-    constexpr int T = kLoBits, H = wave_bits(T);
-    using TL = Tile<F, T, H, C>;
+__global__ void __launch_bounds__(64 << wave_bits(kLoBits), 4) k_enc_lo(EncArgs a) {
+    constexpr int T = kLoBits;
+    using TL = Tile<F, T, reg_bits(T), C>;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    WindowFor<F> win = make_window<F>(lds + tile_lds_dwords<F, T>(), blockIdx.y << T, 0, 1u << T);
     const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const uint64_t q0 = lane_units(lane);
     const bool live = q0 < a.nunits;
-    const uint64_t ql = live ? q0 : a.nunits - C;  // dead lanes re-read a valid unit: loads stay unpredicated
+    const uint64_t ql = live ? q0 : a.nunits - C;
     const unsigned m = 1u << a.Tm;
     const unsigned c = blockIdx.z, base = c * m;
     const PieceSpace ps{0, 0, blockIdx.y << T};
@@ -99,11 +117,12 @@ __global__ void __launch_bounds__(64 << wave_bits(kLoBits)) k_enc_lo(EncArgs a) 
         const unsigned g = ps.global(TL::piece(0, r, w));
         load_or_zero<F>(x[r], a.in, base + g < a.K, base + g, a.zeros, ql);
     }
-    TL::ifft(x, w, lane, lds, ps, a.skew + (m - 1 + base), a.tabs);
+    win.fill(a.sktab, int(m - 1 + base));
+    TL::ifft(x, w, lane, lds, ps, win);
     if (!live) return;
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) {
-        const unsigned g = ps.global(TL::piece(1, r, w));
+        const unsigned g = ps.global(TL::piece(TL::kLast, r, w));
         store_units<F, C>(a.slab_out.ptr(base + g), q0, x[r]);
     }
 }
@@ -111,14 +130,14 @@ __global__ void __launch_bounds__(64 << wave_bits(kLoBits)) k_enc_lo(EncArgs a) 
 // pass 2: for every chunk IFFT over the high bits and accumulate; then the
 // FFT over the high bits -> slab_out[g]
 template <class F, int T>
-__global__ void __launch_bounds__(64 << wave_bits(T)) k_enc_hi(EncArgs a) {
-    constexpr int H = wave_bits(T);
-    using TL = Tile<F, T, H, C>;
+__global__ void __launch_bounds__(64 << wave_bits(T), 4) k_enc_hi(EncArgs a) {
+    using TL = Tile<F, T, reg_bits(T), C>;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    WindowFor<F> win = make_window<F>(lds + tile_lds_dwords<F, T>(), 0, kLoBits, 1u << T);
     const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const uint64_t q0 = lane_units(lane);
     const bool live = q0 < a.nunits;
-    const uint64_t ql = live ? q0 : a.nunits - C;  // dead lanes re-read a valid unit: loads stay unpredicated
+    const uint64_t ql = live ? q0 : a.nunits - C;
     const unsigned m = 1u << a.Tm;
     const PieceSpace ps{blockIdx.y, kLoBits, 0};
     typename TL::Reg acc, x;
@@ -127,15 +146,16 @@ __global__ void __launch_bounds__(64 << wave_bits(T)) k_enc_hi(EncArgs a) {
 #pragma unroll
         for (int r = 0; r < TL::NR; ++r) {
             const unsigned tp = TL::piece(0, r, w);
-            const unsigned g = ps.global(tp);
             // low tiles that lie entirely past K were all-zero inputs
-            load_or_zero<F>(x[r], a.slab_in, base + (tp << kLoBits) < a.K, base + g, a.zeros, ql);
+            load_or_zero<F>(x[r], a.slab_in, base + (tp << kLoBits) < a.K, base + ps.global(tp), a.zeros, ql);
         }
-        TL::ifft(x, w, lane, lds, ps, a.skew + (m - 1 + base), a.tabs);
+        win.fill(a.sktab, int(m - 1 + base));
+        TL::ifft(x, w, lane, lds, ps, win);
         if (c == 0) TL::copy(acc, x);
         else TL::xor_into(acc, x);
     }
-    TL::fft(acc, w, lane, lds, ps, a.skew - 1, a.tabs);
+    win.fill(a.sktab, -1);
+    TL::fft(acc, w, lane, lds, ps, win);
     if (!live) return;
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) {
@@ -146,22 +166,21 @@ __global__ void __launch_bounds__(64 << wave_bits(T)) k_enc_hi(EncArgs a) {
 
 // pass 3: FFT over the low bits, keep outputs g < R
 template <class F>
-__global__ void __launch_bounds__(64 << wave_bits(kLoBits)) k_enc_fin(EncArgs a) {
-    constexpr int T = kLoBits, H = wave_bits(T);
-    using TL = Tile<F, T, H, C>;
+__global__ void __launch_bounds__(64 << wave_bits(kLoBits), 4) k_enc_fin(EncArgs a) {
+    constexpr int T = kLoBits;
+    using TL = Tile<F, T, reg_bits(T), C>;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    WindowFor<F> win = make_window<F>(lds + tile_lds_dwords<F, T>(), blockIdx.y << T, 0, 1u << T);
     const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const uint64_t q0 = lane_units(lane);
     const bool live = q0 < a.nunits;
-    const uint64_t ql = live ? q0 : a.nunits - C;  // dead lanes re-read a valid unit: loads stay unpredicated
+    const uint64_t ql = live ? q0 : a.nunits - C;
     const PieceSpace ps{0, 0, blockIdx.y << T};
     typename TL::Reg x;
 #pragma unroll
-    for (int r = 0; r < TL::NR; ++r) {
-        const unsigned g = ps.global(TL::piece(1, r, w));
-        load_units<F, C>(x[r], a.slab_in.ptr(g), ql);
-    }
-    TL::fft(x, w, lane, lds, ps, a.skew - 1, a.tabs);
+    for (int r = 0; r < TL::NR; ++r) load_units<F, C>(x[r], a.slab_in.ptr(ps.global(TL::piece(TL::kLast, r, w))), ql);
+    win.fill(a.sktab, -1);
+    TL::fft(x, w, lane, lds, ps, win);
     if (!live) return;
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) {
@@ -174,158 +193,185 @@ __global__ void __launch_bounds__(64 << wave_bits(kLoBits)) k_enc_fin(EncArgs a)
 
 LDEV bool bit_set(const uint32_t* bits, unsigned p) { return (cload(bits + (p >> 5)) >> (p & 31)) & 1u; }
 
-// Erasure bitmap over codeword positions (bit p <=> error_locations[p] = 1,
-// LeopardFF8.cpp:1825-1840).  FF16 keeps it in device memory.
-struct ErasedDev {
+// FF16 decoder state in device memory: erasure bitmap (bit p <=>
+// error_locations[p] = 1, LeopardFF8.cpp:1825-1840) and error locator logs.
+// Multiply tables by log value come through the scalar cache.
+struct State16 {
     const uint32_t* bits;
-    LDEV bool get(unsigned p) const { return bit_set(bits, p); }
+    const uint32_t* el;
+    const uint32_t* tabs;
+    LDEV bool erased(unsigned p) const { return bit_set(bits, p); }
+    LDEV unsigned loc(unsigned p) const { return cload(el + p); }
+    LDEV FF16::Tab table(unsigned lm) const { return FF16::tab(tabs, lm); }
 };
-
-// Wave-uniform read of the value lane (p & 63) holds in register (p >> 6) of a
-// 4-register per-lane spread (positions lane + 64 j).  Only static register
-// indices and readlane: nothing is spilled to private memory.
-LDEV unsigned spread_at(const unsigned (&v)[4], unsigned p) {
-    const unsigned l = p & 63, j = p >> 6;
-    const unsigned a = __builtin_amdgcn_readlane(v[0], l), b = __builtin_amdgcn_readlane(v[1], l);
-    const unsigned c = __builtin_amdgcn_readlane(v[2], l), d = __builtin_amdgcn_readlane(v[3], l);
-    return j == 0 ? a : j == 1 ? b : j == 2 ? c : d;
-}
 
 // FF8 decoder state computed inside the kernel by every wave: erasure flags
 // and the error locator (LeopardFF8.cpp:1848-1853) for all 256 positions,
-// lane holding positions lane + 64 j.  Fully reduced mod 255 (congruent to
-// the reference's partially reduced values; the multiply tables treat 0 and
-// 255 identically).
-struct Dec8 {
-    unsigned e[4];  // error locator logs
-    unsigned f[4];  // erasure flags
+// lane holding positions lane + 64 j; fully reduced mod 255 (congruent to the
+// reference's partially reduced values; the multiply tables treat 0 and 255
+// identically).  A wave only ever asks about positions of one 64-block (its 16
+// layout-0 positions), so view() picks that register once and each query is
+// a single readlane.  Multiply tables by log value sit in LDS.
+struct State8 {
+    // Named scalars rather than arrays: a select over array elements is turned
+    // into a private-memory (scratch) index by the compiler.
+    unsigned e0, e1, e2, e3;  // error locator logs, positions lane + 64 j
+    unsigned f0, f1, f2, f3;  // erasure flags
+    unsigned ev = 0, fv = 0;
+    const uint32_t* ltab = nullptr;
     LDEV static unsigned addm(unsigned a, unsigned b) { unsigned s = a + b; return s >= 255u ? s - 255u : s; }
     LDEV static unsigned subm(unsigned a, unsigned b) { unsigned s = a + 255u - b; return s >= 255u ? s - 255u : s; }
+    LDEV static void lanes(unsigned& v, unsigned lane, int d) {
+        const unsigned o = __shfl_xor(int(v), d);
+        v = (lane & d) ? subm(o, v) : addm(v, o);
+    }
     LDEV void fwht(unsigned lane) {
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const unsigned o = __shfl_xor(int(e[j]), d);
-                e[j] = (lane & d) ? subm(o, e[j]) : addm(e[j], o);
-            }
+            lanes(e0, lane, d);
+            lanes(e1, lane, d);
+            lanes(e2, lane, d);
+            lanes(e3, lane, d);
         }
-        const unsigned a0 = addm(e[0], e[1]), a1 = subm(e[0], e[1]);
-        const unsigned a2 = addm(e[2], e[3]), a3 = subm(e[2], e[3]);
-        e[0] = addm(a0, a2); e[2] = subm(a0, a2);
-        e[1] = addm(a1, a3); e[3] = subm(a1, a3);
+        const unsigned a0 = addm(e0, e1), a1 = subm(e0, e1);
+        const unsigned a2 = addm(e2, e3), a3 = subm(e2, e3);
+        e0 = addm(a0, a2); e2 = subm(a0, a2);
+        e1 = addm(a1, a3); e3 = subm(a1, a3);
     }
-    LDEV void compute(const uint32_t (&words)[8], const uint32_t* __restrict__ walsh, unsigned lane) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t word = (lane & 32) ? words[2 * j + 1] : words[2 * j];
-            f[j] = (word >> (lane & 31)) & 1u;
-            e[j] = f[j];
-        }
+    LDEV static unsigned bit(uint32_t lo_word, uint32_t hi_word, unsigned lane) {
+        const uint32_t hm = 0u - ((lane >> 5) & 1u);  // all ones for lanes 32..63
+        return (((lo_word & ~hm) | (hi_word & hm)) >> (lane & 31)) & 1u;
+    }
+    LDEV void compute(const DecArgs& a, unsigned lane) {
+        f0 = bit(a.erased8[0], a.erased8[1], lane);
+        f1 = bit(a.erased8[2], a.erased8[3], lane);
+        f2 = bit(a.erased8[4], a.erased8[5], lane);
+        f3 = bit(a.erased8[6], a.erased8[7], lane);
+        e0 = f0; e1 = f1; e2 = f2; e3 = f3;
         fwht(lane);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) e[j] = (e[j] * walsh[lane + 64 * j]) % 255u;
+        const uint32_t* __restrict__ walsh = a.walsh;
+        e0 = (e0 * walsh[lane]) % 255u;
+        e1 = (e1 * walsh[lane + 64]) % 255u;
+        e2 = (e2 * walsh[lane + 128]) % 255u;
+        e3 = (e3 * walsh[lane + 192]) % 255u;
         fwht(lane);
     }
-    LDEV unsigned at(unsigned p) const { return spread_at(e, p); }
-    LDEV bool get(unsigned p) const { return spread_at(f, p) != 0; }
-};
-struct ElDev {
-    const uint32_t* el;
-    LDEV unsigned at(unsigned p) const { return cload(el + p); }
+    LDEV void view(unsigned block) {  // block = position >> 6, wave-uniform
+        const uint32_t m0 = 0u - (block == 0), m1 = 0u - (block == 1), m2 = 0u - (block == 2), m3 = 0u - (block == 3);
+        ev = (e0 & m0) | (e1 & m1) | (e2 & m2) | (e3 & m3);
+        fv = (f0 & m0) | (f1 & m1) | (f2 & m2) | (f3 & m3);
+    }
+    LDEV bool erased(unsigned p) const { return __builtin_amdgcn_readlane(fv, p & 63) != 0; }
+    LDEV unsigned loc(unsigned p) const { return __builtin_amdgcn_readlane(ev, p & 63); }
+    LDEV FF8::Tab table(unsigned lm) const { return FF8::tab_lds(ltab + lm * FF8::kTabDw); }
 };
 
 // Received piece at codeword position p, scaled by exp(el[p]); zero if absent.
 // Positions: [0, m) recovery (only [0, R) exist), [m, m+K) originals
 // (LeopardFF8.cpp:1857-1877).  Branch-free on the vector side: an absent piece
 // reads the zero page at unit 0 through the all-zero multiply table.
-template <class F, class Er, class El>
-LDEV void load_received(uint32_t* x, const DecArgs& a, const Er& erased, const El& el, unsigned p, uint64_t q) {
+template <class F, class St>
+LDEV void load_received(uint32_t* x, const DecArgs& a, const St& st, unsigned p, uint64_t q) {
     const uint8_t* src = a.zeros;
     unsigned lm = F::kModulus + 1;  // the zero table
     uint64_t qq = 0;
-    if (!erased.get(p)) {
-        if (p < a.R) { src = a.rec.ptr(p); lm = el.at(p); qq = q; }
-        else if (p >= a.m && p < a.m + a.K) { src = a.orig.ptr(p - a.m); lm = el.at(p); qq = q; }
+    if (!st.erased(p)) {
+        if (p < a.R) { src = a.rec.ptr(p); lm = st.loc(p); qq = q; }
+        else if (p >= a.m && p < a.m + a.K) { src = a.orig.ptr(p - a.m); lm = st.loc(p); qq = q; }
     }
     uint32_t y[C * F::kDw];
     load_units<F, C>(y, src, qq);
-    const typename F::Tab t = F::tab(a.tabs, lm);
+    const typename F::Tab t = st.table(lm);
 #pragma unroll
     for (int u = 0; u < C; ++u) F::mul(&x[u * F::kDw], &y[u * F::kDw], t);
 }
 
 // Lost original at position p = m + i: work[i] = z[p] * exp(-el[p])  (LeopardFF8.cpp:1913-1915).
-template <class F, class Er, class El>
-LDEV void reveal(const uint32_t* z, const DecArgs& a, const Er& erased, const El& el, unsigned p, uint64_t q0) {
-    if (p >= a.m && p < a.m + a.K && erased.get(p)) {
+template <class F, class St>
+LDEV void reveal(const uint32_t* z, const DecArgs& a, const St& st, unsigned p, uint64_t q0) {
+    if (p >= a.m && p < a.m + a.K && st.erased(p)) {
         uint32_t y[C * F::kDw];
-        const typename F::Tab t = F::tab(a.tabs, F::kModulus - el.at(p));
+        const typename F::Tab t = st.table(F::kModulus - st.loc(p));
 #pragma unroll
         for (int u = 0; u < C; ++u) F::mul(&y[u * F::kDw], &z[u * F::kDw], t);
         store_units<F, C>(a.out.ptr(p - a.m), q0, y);
     }
 }
 
-template <class F, int T>
-__global__ void __launch_bounds__(64 << wave_bits(T)) k_dec_fused(DecArgs a) {
-    constexpr int H = wave_bits(T);
-    using TL = Tile<F, T, H, C>;
+template <int T>
+__global__ void __launch_bounds__(64 << wave_bits(T), 4) k_dec_fused8(DecArgs a) {
+    using F = FF8;
+    using TL = Tile<F, T, reg_bits(T), C>;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    WindowFor<F> win = make_window<F>(lds + tile_lds_dwords<F, T>(), 0, 0, 1u << T);
+    uint32_t* ltab = lds + tile_lds_dwords<F, T>() + window_dwords<F>(1u << T);
     const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const uint64_t q0 = lane_units(lane);
     const bool live = q0 < a.nunits;
-    const uint64_t ql = live ? q0 : a.nunits - C;  // dead lanes re-read a valid unit: loads stay unpredicated
+    const uint64_t ql = live ? q0 : a.nunits - C;
     const PieceSpace ps{0, 0, 0};
-    Dec8 st;
-    st.compute(a.erased8, a.walsh, lane);
-    const Dec8& erased = st;
-    const Dec8& el = st;
+    // log-indexed multiply tables (scaling) into LDS, then the butterfly window
+    for (unsigned i = threadIdx.x; i < kLogTab8Dwords; i += blockDim.x) ltab[i] = a.tabs[i];
+    win.fill(a.sktab, -1);
+    State8 st;
+    st.compute(a, lane);
+    st.ltab = ltab;
+    st.view(uniform(TL::piece(0, 0, w) >> 6));
 
     typename TL::Reg v, z;
 #pragma unroll
-    for (int r = 0; r < TL::NR; ++r) load_received<F>(v[r], a, erased, el, TL::piece(0, r, w), ql);
-    TL::ifft(v, w, lane, lds, ps, a.skew - 1, a.tabs);
+    for (int r = 0; r < TL::NR; ++r) {
+        load_received<F>(v[r], a, st, TL::piece(0, r, w), ql);
+        __builtin_amdgcn_sched_barrier(0);  // one scaling table live at a time
+    }
+    TL::ifft(v, w, lane, lds, ps, win);
     TL::copy(z, v);
     TL::derivative_add(z, v, w, lane, lds);
-    TL::fft(z, w, lane, lds, ps, a.skew - 1, a.tabs);
+    TL::fft(z, w, lane, lds, ps, win);
     if (!live) return;
 #pragma unroll
-    for (int r = 0; r < TL::NR; ++r) reveal<F>(z[r], a, erased, el, TL::piece(0, r, w), q0);
+    for (int r = 0; r < TL::NR; ++r) {
+        reveal<F>(z[r], a, st, TL::piece(0, r, w), q0);
+        __builtin_amdgcn_sched_barrier(0);
+    }
 }
 
 // pass 1: scale-on-load + IFFT over the low bits -> a_out[g]
 template <class F>
-__global__ void __launch_bounds__(64 << wave_bits(kLoBits)) k_dec_lo(DecArgs a) {
-    constexpr int T = kLoBits, H = wave_bits(T);
-    using TL = Tile<F, T, H, C>;
+__global__ void __launch_bounds__(64 << wave_bits(kLoBits), 4) k_dec_lo(DecArgs a) {
+    constexpr int T = kLoBits;
+    using TL = Tile<F, T, reg_bits(T), C>;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    WindowFor<F> win = make_window<F>(lds + tile_lds_dwords<F, T>(), blockIdx.y << T, 0, 1u << T);
     const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const uint64_t q0 = lane_units(lane);
     const bool live = q0 < a.nunits;
-    const uint64_t ql = live ? q0 : a.nunits - C;  // dead lanes re-read a valid unit: loads stay unpredicated
+    const uint64_t ql = live ? q0 : a.nunits - C;
     const PieceSpace ps{0, 0, blockIdx.y << T};
-    const ErasedDev erased{a.erased_dev};
-    const ElDev el{a.el};
+    const State16 st{a.erased_dev, a.el, a.tabs};
     typename TL::Reg v;
 #pragma unroll
-    for (int r = 0; r < TL::NR; ++r) load_received<F>(v[r], a, erased, el, ps.global(TL::piece(0, r, w)), ql);
-    TL::ifft(v, w, lane, lds, ps, a.skew - 1, a.tabs);
+    for (int r = 0; r < TL::NR; ++r) {
+        load_received<F>(v[r], a, st, ps.global(TL::piece(0, r, w)), ql);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    win.fill(a.sktab, -1);
+    TL::ifft(v, w, lane, lds, ps, win);
     if (!live) return;
 #pragma unroll
-    for (int r = 0; r < TL::NR; ++r) store_units<F, C>(a.a_out.ptr(ps.global(TL::piece(1, r, w))), q0, v[r]);
+    for (int r = 0; r < TL::NR; ++r) store_units<F, C>(a.a_out.ptr(ps.global(TL::piece(TL::kLast, r, w))), q0, v[r]);
 }
 
 // pass 2: IFFT over the high bits, a = (I + D_hi) v, write F_hi(a), F_hi(v)
 template <class F, int T>
-__global__ void __launch_bounds__(64 << wave_bits(T)) k_dec_hi(DecArgs a) {
-    constexpr int H = wave_bits(T);
-    using TL = Tile<F, T, H, C>;
+__global__ void __launch_bounds__(64 << wave_bits(T), 4) k_dec_hi(DecArgs a) {
+    using TL = Tile<F, T, reg_bits(T), C>;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    WindowFor<F> win = make_window<F>(lds + tile_lds_dwords<F, T>(), 0, kLoBits, 1u << T);
     const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const uint64_t q0 = lane_units(lane);
     const bool live = q0 < a.nunits;
-    const uint64_t ql = live ? q0 : a.nunits - C;  // dead lanes re-read a valid unit: loads stay unpredicated
+    const uint64_t ql = live ? q0 : a.nunits - C;
     const PieceSpace ps{blockIdx.y, kLoBits, 0};
     typename TL::Reg v, d;
 #pragma unroll
@@ -333,14 +379,15 @@ __global__ void __launch_bounds__(64 << wave_bits(T)) k_dec_hi(DecArgs a) {
         const unsigned tp = TL::piece(0, r, w);
         load_or_zero<F>(v[r], a.a_in, tp < a.nlo, ps.global(tp), a.zeros, ql);
     }
-    TL::ifft(v, w, lane, lds, ps, a.skew - 1, a.tabs);
+    win.fill(a.sktab, -1);
+    TL::ifft(v, w, lane, lds, ps, win);
     TL::copy(d, v);
     TL::derivative_add(d, v, w, lane, lds);
-    TL::fft(d, w, lane, lds, ps, a.skew - 1, a.tabs);
+    TL::fft(d, w, lane, lds, ps, win);
     if (live)
 #pragma unroll
         for (int r = 0; r < TL::NR; ++r) store_units<F, C>(a.a_out.ptr(ps.global(TL::piece(0, r, w))), q0, d[r]);
-    TL::fft(v, w, lane, lds, ps, a.skew - 1, a.tabs);
+    TL::fft(v, w, lane, lds, ps, win);
     if (live)
 #pragma unroll
         for (int r = 0; r < TL::NR; ++r) store_units<F, C>(a.b_out.ptr(ps.global(TL::piece(0, r, w))), q0, v[r]);
@@ -348,37 +395,38 @@ __global__ void __launch_bounds__(64 << wave_bits(T)) k_dec_hi(DecArgs a) {
 
 // pass 3: z = A + D_lo(V), FFT over the low bits, reveal lost originals
 template <class F>
-__global__ void __launch_bounds__(64 << wave_bits(kLoBits)) k_dec_fin(DecArgs a) {
-    constexpr int T = kLoBits, H = wave_bits(T);
-    using TL = Tile<F, T, H, C>;
+__global__ void __launch_bounds__(64 << wave_bits(kLoBits), 4) k_dec_fin(DecArgs a) {
+    constexpr int T = kLoBits;
+    using TL = Tile<F, T, reg_bits(T), C>;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    // skip tiles holding no lost original (uniform across the workgroup)
+    {
+        const unsigned L = T, j = blockIdx.y;
+        if (!((cload(a.needed_pyr + pyr_offset(L) + (j >> 5)) >> (j & 31)) & 1u)) return;
+    }
+    WindowFor<F> win = make_window<F>(lds + tile_lds_dwords<F, T>(), blockIdx.y << T, 0, 1u << T);
     const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const uint64_t q0 = lane_units(lane);
     const bool live = q0 < a.nunits;
-    const uint64_t ql = live ? q0 : a.nunits - C;  // dead lanes re-read a valid unit: loads stay unpredicated
+    const uint64_t ql = live ? q0 : a.nunits - C;
     const PieceSpace ps{0, 0, blockIdx.y << T};
-    // skip tiles holding no lost original (uniform across the workgroup)
-    {
-        const unsigned g0 = blockIdx.y << T;
-        unsigned any = 0;
-        for (unsigned i = g0 >> 5; i < (g0 + (1u << T)) >> 5; ++i) any |= cload(a.erased_dev + i);
-        const unsigned lo = a.m, hi = a.m + a.K;
-        if (!any || g0 + (1u << T) <= lo || g0 >= hi) return;
-    }
-    const ErasedDev erased{a.erased_dev};
-    const ElDev el{a.el};
+    const State16 st{a.erased_dev, a.el, a.tabs};
     typename TL::Reg z, v;
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) {
-        const unsigned g = ps.global(TL::piece(1, r, w));
+        const unsigned g = ps.global(TL::piece(TL::kLast, r, w));
         load_units<F, C>(z[r], a.a_in.ptr(g), ql);
         load_units<F, C>(v[r], a.b_in.ptr(g), ql);
     }
+    win.fill(a.sktab, -1);
     TL::derivative_add(z, v, w, lane, lds);
-    TL::fft(z, w, lane, lds, ps, a.skew - 1, a.tabs);
+    TL::fft(z, w, lane, lds, ps, win);
     if (!live) return;
 #pragma unroll
-    for (int r = 0; r < TL::NR; ++r) reveal<F>(z[r], a, erased, el, ps.global(TL::piece(0, r, w)), q0);
+    for (int r = 0; r < TL::NR; ++r) {
+        reveal<F>(z[r], a, st, ps.global(TL::piece(0, r, w)), q0);
+        __builtin_amdgcn_sched_barrier(0);
+    }
 }
 
 // FF16 error locator over 65536 positions as a 256 x 256 Walsh-Hadamard
@@ -453,38 +501,50 @@ __global__ void __launch_bounds__(256) k_xor_reduce(XorArgs a) {
 unsigned tiles_for(uint64_t nunits) { return unsigned((nunits + kUnitsPerTile - 1) / kUnitsPerTile); }
 
 template <class KernelFn>
-hipError_t launch(KernelFn* fn, dim3 grid, unsigned threads, size_t lds, hipStream_t s, const void* args_ptr,
-                  size_t args_size) {
+hipError_t launch(KernelFn* fn, dim3 grid, unsigned threads, size_t lds_dwords, hipStream_t s, const void* args_ptr) {
+    const size_t lds = lds_dwords * 4;
     if (lds > 65536) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
         if (e != hipSuccess) return e;
     }
-    (void)args_size;
     void* params[] = {const_cast<void*>(args_ptr)};
     return hipLaunchKernel(reinterpret_cast<const void*>(fn), grid, dim3(threads), params, lds, s);
 }
 
 template <class F, int T>
-hipError_t enc_fused_t(const EncArgs& a, hipStream_t s) {
-    return launch(&k_enc_fused<F, T>, dim3(tiles_for(a.nunits)), 64u << wave_bits(T), tile_lds_bytes<F, T>(), s, &a,
-                  sizeof(a));
+constexpr size_t full_tile_lds() {  // transpose area + a window of 2^T entries
+    return tile_lds_dwords<F, T>() + window_dwords<F>(1u << T);
 }
+
 template <class F, int T>
-hipError_t dec_fused_t(const DecArgs& a, hipStream_t s) {
-    return launch(&k_dec_fused<F, T>, dim3(tiles_for(a.nunits)), 64u << wave_bits(T), tile_lds_bytes<F, T>(), s, &a,
-                  sizeof(a));
-}
+struct EncFusedFn {
+    static hipError_t run(const EncArgs& a, hipStream_t s) {
+        return launch(&k_enc_fused<F, T>, dim3(tiles_for(a.nunits)), 64u << wave_bits(T), full_tile_lds<F, T>(), s,
+                      &a);
+    }
+};
 template <class F, int T>
-hipError_t enc_hi_t(const EncArgs& a, hipStream_t s) {
-    return launch(&k_enc_hi<F, T>, dim3(tiles_for(a.nunits), 1u << kLoBits), 64u << wave_bits(T),
-                  tile_lds_bytes<F, T>(), s, &a, sizeof(a));
-}
+struct DecFused8Fn {
+    static hipError_t run(const DecArgs& a, hipStream_t s) {
+        return launch(&k_dec_fused8<T>, dim3(tiles_for(a.nunits)), 64u << wave_bits(T),
+                      full_tile_lds<FF8, T>() + kLogTab8Dwords, s, &a);
+    }
+};
 template <class F, int T>
-hipError_t dec_hi_t(const DecArgs& a, hipStream_t s) {
-    return launch(&k_dec_hi<F, T>, dim3(tiles_for(a.nunits), 1u << kLoBits), 64u << wave_bits(T),
-                  tile_lds_bytes<F, T>(), s, &a, sizeof(a));
-}
+struct EncHiFn {
+    static hipError_t run(const EncArgs& a, hipStream_t s) {
+        return launch(&k_enc_hi<F, T>, dim3(tiles_for(a.nunits), 1u << kLoBits), 64u << wave_bits(T),
+                      full_tile_lds<F, T>(), s, &a);
+    }
+};
+template <class F, int T>
+struct DecHiFn {
+    static hipError_t run(const DecArgs& a, hipStream_t s) {
+        return launch(&k_dec_hi<F, T>, dim3(tiles_for(a.nunits), 1u << kLoBits), 64u << wave_bits(T),
+                      full_tile_lds<F, T>(), s, &a);
+    }
+};
 
 template <template <class, int> class Fn, class F, int TMIN, int TMAX, class A>
 hipError_t dispatch_T(unsigned T, const A& a, hipStream_t s) {
@@ -494,14 +554,6 @@ hipError_t dispatch_T(unsigned T, const A& a, hipStream_t s) {
     });
     return e;
 }
-template <class F, int T>
-struct EncFusedFn { static hipError_t run(const EncArgs& a, hipStream_t s) { return enc_fused_t<F, T>(a, s); } };
-template <class F, int T>
-struct DecFusedFn { static hipError_t run(const DecArgs& a, hipStream_t s) { return dec_fused_t<F, T>(a, s); } };
-template <class F, int T>
-struct EncHiFn { static hipError_t run(const EncArgs& a, hipStream_t s) { return enc_hi_t<F, T>(a, s); } };
-template <class F, int T>
-struct DecHiFn { static hipError_t run(const DecArgs& a, hipStream_t s) { return dec_hi_t<F, T>(a, s); } };
 
 }  // namespace
 
@@ -512,7 +564,7 @@ hipError_t launch_encode_fused(int ff16, unsigned T, const EncArgs& a, hipStream
 hipError_t launch_encode_lo(const EncArgs& a, hipStream_t s) {
     const unsigned m = 1u << a.Tm;
     return launch(&k_enc_lo<FF16>, dim3(tiles_for(a.nunits), m >> kLoBits, a.nchunks), 64u << wave_bits(kLoBits),
-                  tile_lds_bytes<FF16, kLoBits>(), s, &a, sizeof(a));
+                  full_tile_lds<FF16, kLoBits>(), s, &a);
 }
 hipError_t launch_encode_hi(const EncArgs& a, hipStream_t s) {
     return dispatch_T<EncHiFn, FF16, 1, 8>(a.Tm - kLoBits, a, s);
@@ -520,14 +572,14 @@ hipError_t launch_encode_hi(const EncArgs& a, hipStream_t s) {
 hipError_t launch_encode_fin(const EncArgs& a, hipStream_t s) {
     const unsigned tiles = (a.R + (1u << kLoBits) - 1) >> kLoBits;
     return launch(&k_enc_fin<FF16>, dim3(tiles_for(a.nunits), tiles), 64u << wave_bits(kLoBits),
-                  tile_lds_bytes<FF16, kLoBits>(), s, &a, sizeof(a));
+                  full_tile_lds<FF16, kLoBits>(), s, &a);
 }
 hipError_t launch_decode_fused8(unsigned T, const DecArgs& a, hipStream_t s) {
-    return dispatch_T<DecFusedFn, FF8, 1, 8>(T, a, s);
+    return dispatch_T<DecFused8Fn, FF8, 1, 8>(T, a, s);
 }
 hipError_t launch_decode_lo(const DecArgs& a, hipStream_t s) {
     return launch(&k_dec_lo<FF16>, dim3(tiles_for(a.nunits), a.nlo), 64u << wave_bits(kLoBits),
-                  tile_lds_bytes<FF16, kLoBits>(), s, &a, sizeof(a));
+                  full_tile_lds<FF16, kLoBits>(), s, &a);
 }
 hipError_t launch_decode_hi(const DecArgs& a, hipStream_t s) {
     return dispatch_T<DecHiFn, FF16, 1, 8>(a.Tn - kLoBits, a, s);
@@ -535,7 +587,7 @@ hipError_t launch_decode_hi(const DecArgs& a, hipStream_t s) {
 hipError_t launch_decode_fin(const DecArgs& a, hipStream_t s) {
     const unsigned n = 1u << a.Tn;
     return launch(&k_dec_fin<FF16>, dim3(tiles_for(a.nunits), n >> kLoBits), 64u << wave_bits(kLoBits),
-                  tile_lds_bytes<FF16, kLoBits>(), s, &a, sizeof(a));
+                  full_tile_lds<FF16, kLoBits>(), s, &a);
 }
 hipError_t launch_error_locator16(const uint32_t* erased, const uint32_t* walsh, uint32_t* tmp, uint32_t* el,
                                   hipStream_t s) {

@@ -28,7 +28,7 @@
 // Ablation switches for performance experiments only (tools/ablate.sh builds
 // separate libraries with them; the shipped library has LAMD_ABLATE == 0):
 // 1 = no butterfly arithmetic, 2 = no LDS transposes, 4 = no piece loads,
-// 8 = no piece stores.
+// 8 = no piece stores, 16 = fused kernels return at once (launch floor).
 #ifndef LAMD_ABLATE
 #define LAMD_ABLATE 0
 #endif
@@ -171,6 +171,19 @@ LDEV uint64_t unit_offset(uint64_t q) {
     else return (q >> 3) * 64 + (q & 7) * 4;
 }
 
+// Piece memory is global (HBM): say so, or a pointer chosen at run time
+// becomes a flat access, which also counts against lgkmcnt and so makes every
+// later scalar-load wait block on the HBM load as well.
+#if defined(__HIP_DEVICE_COMPILE__)
+template <class V, class P>
+LDEV __attribute__((address_space(1))) V* gptr(P* p) {
+    return (__attribute__((address_space(1))) V*)(p);
+}
+#else
+template <class V, class P>
+LDEV V* gptr(P* p) { return (V*)(p); }
+#endif
+
 template <int C>
 struct VecT;
 template <>
@@ -183,7 +196,7 @@ struct VecT<4> { using type = uint4; };
 template <int C>
 LDEV void vload(uint32_t* dst, const uint8_t* src) {
     using V = typename VecT<C>::type;
-    const V v = *reinterpret_cast<const V*>(src);
+    const V v = *gptr<const V>(src);
     if constexpr (C == 1) dst[0] = v;
     else if constexpr (C == 2) { dst[0] = v.x; dst[1] = v.y; }
     else { dst[0] = v.x; dst[1] = v.y; dst[2] = v.z; dst[3] = v.w; }
@@ -195,7 +208,7 @@ LDEV void vstore(uint8_t* dst, const uint32_t* src) {
     if constexpr (C == 1) v = src[0];
     else if constexpr (C == 2) { v.x = src[0]; v.y = src[1]; }
     else { v.x = src[0]; v.y = src[1]; v.z = src[2]; v.w = src[3]; }
-    *reinterpret_cast<V*>(dst) = v;
+    *gptr<V>(dst) = v;
 }
 
 // One lane's C units of one piece, register layout: for FF8 x[u]; for FF16
@@ -241,45 +254,73 @@ LDEV void store_units(uint8_t* piece, uint64_t q0, const uint32_t* x) {
 
 // Butterfly tables of one transform stage.  A stage with skew base `off`
 // needs the skew-indexed entries off + cidx for the group indices cidx its tile
-// produces.
+// produces (gf_tables.h: build_skew_tables).
 //
-// LdsWindow (FF8: 5-dword tables) stages them in LDS: slot (cidx - base) >>
-// shift holds entry off + cidx.  Whole-transform tiles: base 0, shift 0; tiles
-// of the low 8 bits (other bits fixed to y): base y << 8; tiles of the high
-// bits: cidx is a multiple of 256, shift 8.  Tables land in VGPRs (ds_read),
-// so v_perm needs no SGPR->VGPR copies.
+// LdsSkew8 (FF8, 5-dword tables): the whole 256-entry array is staged once per
+// workgroup in LDS (TabStage8, 5 KB) before the first barrier; a stage only
+// moves the base.  Tables land in VGPRs (ds_read), so v_perm needs no
+// SGPR->VGPR copies and no per-stage refill barrier exists.
 //
-// GlobalWindow (FF16: 20-dword tables) reads entries straight from the global
-// skew-indexed array through the scalar cache (20 SGPRs per table).
-template <class F>
-struct LdsWindow {
-    uint32_t* lds;
-    unsigned base, shift, count;
-    LDEV typename F::Tab table(unsigned cidx) const {
-        return F::tab_lds(lds + ((cidx - base) >> shift) * F::kTabDw);
+// GlobalWindow (FF16, 20-dword tables over 65536 entries) reads entries
+// straight from the global skew-indexed array through the scalar cache.
+// FF8 multiply tables of N entries in LDS, split for a compact footprint (20
+// bytes per entry instead of the 32 of the global layout): the four perm dwords
+// (a0, a1, b0, b1) of entry i as one 16-byte slot, the fifth (c0) in a second
+// array.  Two aligned reads per table (ds_read_b128 + ds_read_b32).
+template <unsigned N>
+struct LdsTab8 {
+    uint32_t* base;
+    static constexpr size_t kDwords = 5 * size_t(N);
+    LDEV FF8::Tab at(int i) const {
+        const uint4 v = reinterpret_cast<const uint4*>(base)[i];
+        return FF8::Tab{v.x, v.y, v.z, v.w, base[4 * N + i]};
     }
-    // Cooperative refill by the whole workgroup (barriers on both sides).
-    LDEV void fill(const uint32_t* sktab, int off) {
-        __syncthreads();
-        const unsigned total = count * F::kTabDw;
-        for (unsigned i = threadIdx.x; i < total; i += blockDim.x) {
-            const unsigned slot = i / F::kTabDw, d = i - slot * F::kTabDw;
-            const long g = long(off) + long(base) + (long(slot) << shift);
-            lds[i] = (g >= 0 && g < long(F::kOrder)) ? sktab[size_t(g) * F::kTabDw + d] : 0u;
-        }
-        __syncthreads();
-    }
-    static constexpr size_t lds_dwords(unsigned count) { return size_t(count) * F::kTabDw; }
+};
+
+struct LdsSkew8 {
+    LdsTab8<256> tabs;
+    int off = 0;
+    LDEV FF8::Tab table(unsigned cidx) const { return tabs.at(off + int(cidx)); }
+    LDEV void stage(const uint32_t*, int o) { off = o; }
 };
 template <class F>
 struct GlobalWindow {
     const uint32_t* sk = nullptr;
     LDEV typename F::Tab table(unsigned cidx) const { return F::tab_at(sk + size_t(cidx) * F::kTabDw); }
-    LDEV void fill(const uint32_t* sktab, int off) { sk = sktab + ptrdiff_t(off) * ptrdiff_t(F::kTabDw); }
-    static constexpr size_t lds_dwords(unsigned) { return 0; }
+    LDEV void stage(const uint32_t* sktab, int off) { sk = sktab + ptrdiff_t(off) * ptrdiff_t(F::kTabDw); }
 };
-template <class F>
-using WindowFor = typename std::conditional<F::kDw == 1, LdsWindow<F>, GlobalWindow<F>>::type;
+
+// Workgroup-cooperative copy of N global FF8 tables (8-dword entries) into an
+// LdsTab8<N>, split so that the global loads are issued first (ahead of the
+// piece loads: vmcnt retires in order, so waiting for these does not wait for
+// the pieces) and the LDS stores happen after the piece loads are in flight.
+template <int NT, unsigned N>
+struct TabStage8 {
+    static constexpr unsigned PER = (N + NT - 1) / NT;  // entries per thread
+    uint4 va[PER];
+    uint32_t vc[PER];
+    LDEV void load(const uint32_t* src) {
+        static_for<0, int(PER)>([&](auto I) __attribute__((always_inline)) {
+            constexpr unsigned i = decltype(I)::value;
+            unsigned e = threadIdx.x + i * NT;
+            if constexpr ((i + 1) * NT > N) e = e < N ? e : N - 1;  // tail: re-read a valid entry
+            va[i] = reinterpret_cast<const uint4*>(src)[2 * e];
+            vc[i] = src[8 * e + 4];
+        });
+    }
+    template <unsigned M>
+    LDEV void store(LdsTab8<M> dst) const {
+        static_assert(M >= N, "destination too small");
+        static_for<0, int(PER)>([&](auto I) __attribute__((always_inline)) {
+            constexpr unsigned i = decltype(I)::value;
+            const unsigned e = threadIdx.x + i * NT;
+            if ((i + 1) * NT <= N || e < N) {
+                reinterpret_cast<uint4*>(dst.base)[e] = va[i];
+                dst.base[4 * M + e] = vc[i];
+            }
+        });
+    }
+};
 
 // Global piece index of tile piece tp:  lo_fixed | tp << l0 | hi_fixed.
 struct PieceSpace {
@@ -324,6 +365,15 @@ struct Tile {
         for (int r = 0; r < NR; ++r)
 #pragma unroll
             for (int k = 0; k < U; ++k) x[r][k] = 0;
+    }
+    // Materialise x here: keeps the compiler from sinking the computation of a
+    // register into the (conditional) blocks that consume it, which would keep
+    // all of its inputs live until then.
+    LDEV static void pin(Reg& x) {
+#pragma unroll
+        for (int r = 0; r < NR; ++r)
+#pragma unroll
+            for (int k = 0; k < U; ++k) asm volatile("" : "+v"(x[r][k]));
     }
     LDEV static void xor_into(Reg& x, const Reg& y) {
 #pragma unroll
@@ -378,10 +428,18 @@ struct Tile {
         if constexpr (F::kDw == 1) {
             // FF8 (5-dword tables): read every table of the layer, then let the
             // scheduler interleave the layer's independent butterflies (ILP).
-            typename F::Tab tabs[NG];
-            static_for<0, NG>([&](auto GI) { tabs[GI.value] = table(GI.value * 2 * half); });
-            static_for<0, NG>([&](auto GI) { group(GI.value * 2 * half, tabs[GI.value]); });
-            __builtin_amdgcn_sched_barrier(0);  // keep the next layer's tables below this one
+            // At most 4 tables (20 VGPRs) live at a time.
+            constexpr int KB = NG < 4 ? NG : 4;
+            static_for<0, NG / KB>([&](auto BI) {
+                constexpr int g0 = decltype(BI)::value * KB;
+                typename F::Tab tabs[KB];
+                // Re-read tables from LDS each time rather than let the compiler
+                // keep earlier reads of the same entries live across the transform.
+                asm volatile("" ::: "memory");
+                static_for<0, KB>([&](auto GI) { tabs[GI.value] = table((g0 + GI.value) * 2 * half); });
+                static_for<0, KB>([&](auto GI) { group((g0 + GI.value) * 2 * half, tabs[GI.value]); });
+                __builtin_amdgcn_sched_barrier(0);  // keep the next batch's tables below this one
+            });
         } else {
             // FF16 (20-dword tables in SGPRs): software pipeline, two tables live.
             typename F::Tab next = table(0);
@@ -437,6 +495,41 @@ struct Tile {
             });
             if constexpr (k > 0) transpose<k, k - 1>(x, w, lane, lds);
         });
+    }
+
+    // v = (I + D) v in place: the derivative of a transform that fits the tile
+    // (layout kLast).  Register bits: ascending r reads v[r | 2^b] before it is
+    // modified; wave bits: gathered from an LDS copy of the original v.
+    LDEV static void derivative_inplace(Reg& v, unsigned w, unsigned lane, uint32_t* lds) {
+        if constexpr (T > R) {
+            __syncthreads();
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                uint32_t* p = lds + (size_t(piece(kLast, r, w)) * 64 + lane) * U;
+#pragma unroll
+                for (int k = 0; k < U; ++k) p[k] = v[r][k];
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < NR; ++r)
+#pragma unroll
+            for (int b = 0; b < R; ++b)
+                if (!(r & (1 << b)))
+#pragma unroll
+                    for (int k = 0; k < U; ++k) v[r][k] ^= v[r | (1 << b)][k];
+        if constexpr (T > R) {
+            __syncthreads();
+            for (int b = 0; b < T - R; ++b) {
+                if (w & (1u << b)) continue;  // wave-uniform
+                const unsigned w2 = w | (1u << b);
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    const uint32_t* p = lds + (size_t(piece(kLast, r, w2)) * 64 + lane) * U;
+#pragma unroll
+                    for (int k = 0; k < U; ++k) v[r][k] ^= p[k];
+                }
+            }
+        }
     }
 
     // d += sum over tile bits b with bit b of k clear of v[k | 2^b]   (layout kLast,

@@ -33,21 +33,32 @@ constexpr int C = kUnitsPerLane;
 constexpr int reg_bits(int T) { return T <= 3 ? T : (T - 3 <= 4 ? 3 : T - 4); }
 constexpr int wave_bits(int T) { return T - reg_bits(T); }
 
-// LDS carve-up: [tile transpose area][butterfly-table window][FF8 decoder: log tables]
+// LDS carve-up: [tile transpose area][FF8: skew tables][FF8 decoder: log tables, error locator]
 template <class F, int T>
 constexpr size_t tile_lds_dwords() {
     return wave_bits(T) > 0 ? (size_t(1) << T) * 64 * C * F::kDw : 0;  // transposes
 }
-template <class F>
-constexpr size_t window_dwords(unsigned entries) {
-    return WindowFor<F>::lds_dwords(entries);
-}
-template <class F>
-LDEV WindowFor<F> make_window(uint32_t* lds, unsigned base, unsigned shift, unsigned count) {
-    if constexpr (F::kDw == 1) return LdsWindow<F>{lds, base, shift, count};
-    else return GlobalWindow<F>{};
-}
-constexpr size_t kLogTab8Dwords = 257 * FF8::kTabDw;
+
+// Butterfly tables of a kernel: FF16 reads them through the scalar cache; FF8
+// stages the whole skew-indexed array into LDS once (TabStage8: global loads
+// issued before the piece loads, LDS stores + the one barrier after them).
+template <class F, int NT>
+struct SkewTables {
+    using Win = GlobalWindow<F>;
+    static constexpr size_t kLdsDwords = 0;
+    LDEV void load(const uint32_t*) {}
+    LDEV void publish(uint32_t*) const {}
+    LDEV static Win window(uint32_t*) { return Win{}; }
+};
+template <int NT>
+struct SkewTables<FF8, NT> {
+    using Win = LdsSkew8;
+    static constexpr size_t kLdsDwords = LdsTab8<256>::kDwords;
+    TabStage8<NT, 256> st;
+    LDEV void load(const uint32_t* sktab) { st.load(sktab); }
+    LDEV void publish(uint32_t* lds) const { st.store(LdsTab8<256>{lds}); }
+    LDEV static Win window(uint32_t* lds) { return Win{LdsTab8<256>{lds}}; }
+};
 
 LDEV uint64_t lane_units(unsigned lane) { return (uint64_t(blockIdx.x) * 64 + lane) * C; }
 
@@ -65,9 +76,14 @@ LDEV void load_or_zero(uint32_t* x, const PieceMap& pm, bool ok, unsigned i, con
 
 template <class F, int T>
 __global__ void __launch_bounds__(64 << wave_bits(T), 4) k_enc_fused(EncArgs a) {
+    if constexpr ((LAMD_ABLATE & 16) != 0) return;
     using TL = Tile<F, T, reg_bits(T), C>;
+    constexpr int NT = 64 << wave_bits(T);
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    WindowFor<F> win = make_window<F>(lds + tile_lds_dwords<F, T>(), 0, 0, 1u << T);
+    uint32_t* sk_lds = lds + tile_lds_dwords<F, T>();
+    SkewTables<F, NT> sk;
+    sk.load(a.sktab);
+    auto win = sk.window(sk_lds);
     const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const uint64_t q0 = lane_units(lane);
     const bool live = q0 < a.nunits;
@@ -75,7 +91,7 @@ __global__ void __launch_bounds__(64 << wave_bits(T), 4) k_enc_fused(EncArgs a) 
     constexpr unsigned m = 1u << T;
     const PieceSpace ps{0, 0, 0};
     typename TL::Reg acc, x;
-    for (unsigned c = 0; c < a.nchunks; ++c) {
+    auto load_chunk = [&](unsigned c) {
         const unsigned base = c * m;
         const unsigned cnt = a.K - base < m ? a.K - base : m;
 #pragma unroll
@@ -83,13 +99,21 @@ __global__ void __launch_bounds__(64 << wave_bits(T), 4) k_enc_fused(EncArgs a) 
             const unsigned tp = TL::piece(0, r, w);
             load_or_zero<F>(x[r], a.in, tp < cnt, base + tp, a.zeros, ql);
         }
-        win.fill(a.sktab, int(m - 1 + base));
+    };
+    load_chunk(0);
+    sk.publish(sk_lds);
+    __syncthreads();
+    TL::zero(acc);
+    for (unsigned c = 0;;) {
+        win.stage(a.sktab, int(m - 1 + c * m));
         TL::ifft(x, w, lane, lds, ps, win);
-        if (c == 0) TL::copy(acc, x);
-        else TL::xor_into(acc, x);
+        TL::xor_into(acc, x);
+        if (++c >= a.nchunks) break;
+        load_chunk(c);
     }
-    win.fill(a.sktab, -1);
+    win.stage(a.sktab, -1);
     TL::fft(acc, w, lane, lds, ps, win);
+    TL::pin(acc);
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) {
         const unsigned tp = TL::piece(0, r, w);
@@ -103,7 +127,7 @@ __global__ void __launch_bounds__(64 << wave_bits(kLoBits), 4) k_enc_lo(EncArgs 
     constexpr int T = kLoBits;
     using TL = Tile<F, T, reg_bits(T), C>;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    WindowFor<F> win = make_window<F>(lds + tile_lds_dwords<F, T>(), blockIdx.y << T, 0, 1u << T);
+    GlobalWindow<F> win;
     const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const uint64_t q0 = lane_units(lane);
     const bool live = q0 < a.nunits;
@@ -117,7 +141,7 @@ __global__ void __launch_bounds__(64 << wave_bits(kLoBits), 4) k_enc_lo(EncArgs 
         const unsigned g = ps.global(TL::piece(0, r, w));
         load_or_zero<F>(x[r], a.in, base + g < a.K, base + g, a.zeros, ql);
     }
-    win.fill(a.sktab, int(m - 1 + base));
+    win.stage(a.sktab, int(m - 1 + base));
     TL::ifft(x, w, lane, lds, ps, win);
     if (!live) return;
 #pragma unroll
@@ -133,7 +157,7 @@ template <class F, int T>
 __global__ void __launch_bounds__(64 << wave_bits(T), 4) k_enc_hi(EncArgs a) {
     using TL = Tile<F, T, reg_bits(T), C>;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    WindowFor<F> win = make_window<F>(lds + tile_lds_dwords<F, T>(), 0, kLoBits, 1u << T);
+    GlobalWindow<F> win;
     const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const uint64_t q0 = lane_units(lane);
     const bool live = q0 < a.nunits;
@@ -149,12 +173,12 @@ __global__ void __launch_bounds__(64 << wave_bits(T), 4) k_enc_hi(EncArgs a) {
             // low tiles that lie entirely past K were all-zero inputs
             load_or_zero<F>(x[r], a.slab_in, base + (tp << kLoBits) < a.K, base + ps.global(tp), a.zeros, ql);
         }
-        win.fill(a.sktab, int(m - 1 + base));
+        win.stage(a.sktab, int(m - 1 + base));
         TL::ifft(x, w, lane, lds, ps, win);
         if (c == 0) TL::copy(acc, x);
         else TL::xor_into(acc, x);
     }
-    win.fill(a.sktab, -1);
+    win.stage(a.sktab, -1);
     TL::fft(acc, w, lane, lds, ps, win);
     if (!live) return;
 #pragma unroll
@@ -170,7 +194,7 @@ __global__ void __launch_bounds__(64 << wave_bits(kLoBits), 4) k_enc_fin(EncArgs
     constexpr int T = kLoBits;
     using TL = Tile<F, T, reg_bits(T), C>;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    WindowFor<F> win = make_window<F>(lds + tile_lds_dwords<F, T>(), blockIdx.y << T, 0, 1u << T);
+    GlobalWindow<F> win;
     const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const uint64_t q0 = lane_units(lane);
     const bool live = q0 < a.nunits;
@@ -179,7 +203,7 @@ __global__ void __launch_bounds__(64 << wave_bits(kLoBits), 4) k_enc_fin(EncArgs
     typename TL::Reg x;
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) load_units<F, C>(x[r], a.slab_in.ptr(ps.global(TL::piece(TL::kLast, r, w))), ql);
-    win.fill(a.sktab, -1);
+    win.stage(a.sktab, -1);
     TL::fft(x, w, lane, lds, ps, win);
     if (!live) return;
 #pragma unroll
@@ -205,66 +229,64 @@ struct State16 {
     LDEV FF16::Tab table(unsigned lm) const { return FF16::tab(tabs, lm); }
 };
 
-// FF8 decoder state computed inside the kernel by every wave: erasure flags
-// and the error locator (LeopardFF8.cpp:1848-1853) for all 256 positions,
-// lane holding positions lane + 64 j; fully reduced mod 255 (congruent to the
-// reference's partially reduced values; the multiply tables treat 0 and 255
-// identically).  A wave only ever asks about positions of one 64-block (its 16
-// layout-0 positions), so view() picks that register once and each query is
-// a single readlane.  Multiply tables by log value sit in LDS.
-struct State8 {
-    // Named scalars rather than arrays: a select over array elements is turned
-    // into a private-memory (scratch) index by the compiler.
-    unsigned e0, e1, e2, e3;  // error locator logs, positions lane + 64 j
-    unsigned f0, f1, f2, f3;  // erasure flags
-    unsigned ev = 0, fv = 0;
-    const uint32_t* ltab = nullptr;
-    LDEV static unsigned addm(unsigned a, unsigned b) { unsigned s = a + b; return s >= 255u ? s - 255u : s; }
-    LDEV static unsigned subm(unsigned a, unsigned b) { unsigned s = a + 255u - b; return s >= 255u ? s - 255u : s; }
-    LDEV static void lanes(unsigned& v, unsigned lane, int d) {
-        const unsigned o = __shfl_xor(int(v), d);
-        v = (lane & d) ? subm(o, v) : addm(v, o);
-    }
-    LDEV void fwht(unsigned lane) {
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            lanes(e0, lane, d);
-            lanes(e1, lane, d);
-            lanes(e2, lane, d);
-            lanes(e3, lane, d);
+// FF8 error locator (LeopardFF8.cpp:1848-1853), computed inside the decode
+// kernel by wave 0 while the piece loads of all waves are in flight:
+// el = FWHT(LogWalsh * FWHT(erasures)) mod 255 for the 256 positions, lane
+// holding positions lane + 64 j, written to LDS.
+//
+// The transforms run on plain signed integers and reduce once at the end:
+// every step is congruent mod 255 to the reference's mod-255 butterflies
+// (|values| stay below 2^25).  Results are fully reduced (0..254), congruent
+// to the reference's partially reduced ones; the multiply tables treat log 0
+// and log 255 identically.  Cross-lane partners come from DPP (lane ^ 1..8)
+// and the gfx950 permlane swaps (lane ^ 16, 32): VALU only, no LDS round trip.
+struct El8 {
+    template <int D>
+    LDEV static int partner(int v, unsigned lane) {
+        if constexpr (D == 1) return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+        else if constexpr (D == 2) return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);  // [2,3,0,1]
+        else if constexpr (D == 4)  // quad_perm [3,2,1,0] (^3), then row_half_mirror (^7)
+            return __builtin_amdgcn_mov_dpp(__builtin_amdgcn_mov_dpp(v, 0x1B, 0xF, 0xF, false), 0x141, 0xF, 0xF, false);
+        else if constexpr (D == 8)  // row_mirror (^15), then row_half_mirror (^7)
+            return __builtin_amdgcn_mov_dpp(__builtin_amdgcn_mov_dpp(v, 0x140, 0xF, 0xF, false), 0x141, 0xF, 0xF, false);
+        else if constexpr (D == 16) {
+            const auto r = __builtin_amdgcn_permlane16_swap(unsigned(v), unsigned(v), false, false);
+            return int((lane & 16u) ? r[0] : r[1]);
+        } else {
+            const auto r = __builtin_amdgcn_permlane32_swap(unsigned(v), unsigned(v), false, false);
+            return int((lane & 32u) ? r[0] : r[1]);
         }
-        const unsigned a0 = addm(e0, e1), a1 = subm(e0, e1);
-        const unsigned a2 = addm(e2, e3), a3 = subm(e2, e3);
-        e0 = addm(a0, a2); e2 = subm(a0, a2);
-        e1 = addm(a1, a3); e3 = subm(a1, a3);
     }
-    LDEV static unsigned bit(uint32_t lo_word, uint32_t hi_word, unsigned lane) {
-        const uint32_t hm = 0u - ((lane >> 5) & 1u);  // all ones for lanes 32..63
-        return (((lo_word & ~hm) | (hi_word & hm)) >> (lane & 31)) & 1u;
+    // (a, b) -> (a + b, a - b) on every pair of positions differing in one bit
+    LDEV static void fwht(int (&e)[4], unsigned lane) {
+        static_for<0, 6>([&](auto I) {
+            constexpr int D = 1 << decltype(I)::value;
+            int o[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[j] = partner<D>(e[j], lane);
+            const bool upper = (lane & unsigned(D)) != 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) e[j] = upper ? o[j] - e[j] : e[j] + o[j];
+        });
+        const int a0 = e[0] + e[1], a1 = e[0] - e[1], a2 = e[2] + e[3], a3 = e[2] - e[3];
+        e[0] = a0 + a2; e[2] = a0 - a2;
+        e[1] = a1 + a3; e[3] = a1 - a3;
     }
-    LDEV void compute(const DecArgs& a, unsigned lane) {
-        f0 = bit(a.erased8[0], a.erased8[1], lane);
-        f1 = bit(a.erased8[2], a.erased8[3], lane);
-        f2 = bit(a.erased8[4], a.erased8[5], lane);
-        f3 = bit(a.erased8[6], a.erased8[7], lane);
-        e0 = f0; e1 = f1; e2 = f2; e3 = f3;
-        fwht(lane);
-        const uint32_t* __restrict__ walsh = a.walsh;
-        e0 = (e0 * walsh[lane]) % 255u;
-        e1 = (e1 * walsh[lane + 64]) % 255u;
-        e2 = (e2 * walsh[lane + 128]) % 255u;
-        e3 = (e3 * walsh[lane + 192]) % 255u;
-        fwht(lane);
+    LDEV static void compute(const DecArgs& a, const unsigned (&walsh)[4], unsigned lane, uint32_t* el_lds) {
+        int e[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) e[j] = int((a.erased8[2 * j + (lane >> 5)] >> (lane & 31)) & 1u);
+        fwht(e, lane);  // |e| <= 256
+#pragma unroll
+        for (int j = 0; j < 4; ++j) e[j] = int((unsigned(e[j] + 510) % 255u) * walsh[j]);  // < 2^16
+        fwht(e, lane);  // |e| < 2^24
+#pragma unroll
+        for (int j = 0; j < 4; ++j) el_lds[lane + 64 * j] = unsigned(e[j] + 255 * 65536) % 255u;
     }
-    LDEV void view(unsigned block) {  // block = position >> 6, wave-uniform
-        const uint32_t m0 = 0u - (block == 0), m1 = 0u - (block == 1), m2 = 0u - (block == 2), m3 = 0u - (block == 3);
-        ev = (e0 & m0) | (e1 & m1) | (e2 & m2) | (e3 & m3);
-        fv = (f0 & m0) | (f1 & m1) | (f2 & m2) | (f3 & m3);
-    }
-    LDEV bool erased(unsigned p) const { return __builtin_amdgcn_readlane(fv, p & 63) != 0; }
-    LDEV unsigned loc(unsigned p) const { return __builtin_amdgcn_readlane(ev, p & 63); }
-    LDEV FF8::Tab table(unsigned lm) const { return FF8::tab_lds(ltab + lm * FF8::kTabDw); }
 };
+
+// Erasure bit of codeword position p (wave-uniform) from the by-value bitmap.
+LDEV bool erased8(const DecArgs& a, unsigned p) { return (a.erased8[p >> 5] >> (p & 31)) & 1u; }
 
 // Received piece at codeword position p, scaled by exp(el[p]); zero if absent.
 // Positions: [0, m) recovery (only [0, R) exist), [m, m+K) originals
@@ -298,41 +320,77 @@ LDEV void reveal(const uint32_t* z, const DecArgs& a, const St& st, unsigned p, 
     }
 }
 
+// Whole FF8 decode in one tile (n <= 256):
+//   prologue: table loads (global) -> piece loads -> tables to LDS, wave 0
+//             computes the error locator into LDS -> one barrier;
+//   scale received pieces by exp(el) (LeopardFF8.cpp:1857-1877), IFFT,
+//   formal derivative (closed form), FFT, reveal lost originals * exp(-el).
 template <int T>
 __global__ void __launch_bounds__(64 << wave_bits(T), 4) k_dec_fused8(DecArgs a) {
+    if constexpr ((LAMD_ABLATE & 16) != 0) return;
     using F = FF8;
     using TL = Tile<F, T, reg_bits(T), C>;
+    constexpr int NT = 64 << wave_bits(T);
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    WindowFor<F> win = make_window<F>(lds + tile_lds_dwords<F, T>(), 0, 0, 1u << T);
-    uint32_t* ltab = lds + tile_lds_dwords<F, T>() + window_dwords<F>(1u << T);
+    const LdsTab8<256> sk_tabs{lds + tile_lds_dwords<F, T>()};
+    const LdsTab8<257> ltab{sk_tabs.base + LdsTab8<256>::kDwords};  // by log value, 256 = zero
+    uint32_t* el = ltab.base + LdsTab8<257>::kDwords;
     const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    TabStage8<NT, 256> sk_stage;
+    TabStage8<NT, 256> log_stage;  // entry 256 (the zero table) is written directly
+    sk_stage.load(a.sktab);
+    log_stage.load(a.tabs);
+    unsigned walsh[4] = {0, 0, 0, 0};
+    if (w == 0)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) walsh[j] = a.walsh[lane + 64 * j];
     const uint64_t q0 = lane_units(lane);
     const bool live = q0 < a.nunits;
     const uint64_t ql = live ? q0 : a.nunits - C;
     const PieceSpace ps{0, 0, 0};
-    // log-indexed multiply tables (scaling) into LDS, then the butterfly window
-    for (unsigned i = threadIdx.x; i < kLogTab8Dwords; i += blockDim.x) ltab[i] = a.tabs[i];
-    win.fill(a.sktab, -1);
-    State8 st;
-    st.compute(a, lane);
-    st.ltab = ltab;
-    st.view(uniform(TL::piece(0, 0, w) >> 6));
+    LdsSkew8 win{sk_tabs};
 
-    typename TL::Reg v, z;
+    // received pieces: [0, m) recovery (only [0, R) exist), [m, m+K) originals
+    typename TL::Reg v;
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) {
-        load_received<F>(v[r], a, st, TL::piece(0, r, w), ql);
-        __builtin_amdgcn_sched_barrier(0);  // one scaling table live at a time
+        const unsigned p = TL::piece(0, r, w);
+        const uint8_t* src = a.zeros;
+        uint64_t qq = 0;
+        if (!erased8(a, p)) {
+            if (p < a.R) { src = a.rec.ptr(p); qq = ql; }
+            else if (p >= a.m && p < a.m + a.K) { src = a.orig.ptr(p - a.m); qq = ql; }
+        }
+        load_units<F, C>(v[r], src, qq);
     }
+    sk_stage.store(sk_tabs);
+    log_stage.store(ltab);
+    if (threadIdx.x == 0) {
+        reinterpret_cast<uint4*>(ltab.base)[256] = make_uint4(0, 0, 0, 0);
+        ltab.base[4 * 257 + 256] = 0;
+    }
+    if (w == 0) El8::compute(a, walsh, lane, el);
+    __syncthreads();
+    // absent pieces are zero: scaling them by anything keeps them zero
+#pragma unroll
+    for (int r = 0; r < TL::NR; ++r) {
+        F::mul(v[r], v[r], ltab.at(int(el[TL::piece(0, r, w)])));
+    }
+    win.stage(nullptr, -1);
     TL::ifft(v, w, lane, lds, ps, win);
-    TL::copy(z, v);
-    TL::derivative_add(z, v, w, lane, lds);
-    TL::fft(z, w, lane, lds, ps, win);
+    TL::derivative_inplace(v, w, lane, lds);
+    TL::fft(v, w, lane, lds, ps, win);
+    TL::pin(v);
     if (!live) return;
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) {
-        reveal<F>(z[r], a, st, TL::piece(0, r, w), q0);
-        __builtin_amdgcn_sched_barrier(0);
+        const unsigned p = TL::piece(0, r, w);
+        if (p >= a.m && p < a.m + a.K && erased8(a, p)) {  // LeopardFF8.cpp:1913-1915
+            uint32_t y[C];
+            F::mul(y, v[r], ltab.at(int(F::kModulus - el[p])));
+            store_units<F, C>(a.out.ptr(p - a.m), q0, y);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // no hoisting of later pieces' addresses
     }
 }
 
@@ -342,7 +400,7 @@ __global__ void __launch_bounds__(64 << wave_bits(kLoBits), 4) k_dec_lo(DecArgs 
     constexpr int T = kLoBits;
     using TL = Tile<F, T, reg_bits(T), C>;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    WindowFor<F> win = make_window<F>(lds + tile_lds_dwords<F, T>(), blockIdx.y << T, 0, 1u << T);
+    GlobalWindow<F> win;
     const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const uint64_t q0 = lane_units(lane);
     const bool live = q0 < a.nunits;
@@ -355,7 +413,7 @@ __global__ void __launch_bounds__(64 << wave_bits(kLoBits), 4) k_dec_lo(DecArgs 
         load_received<F>(v[r], a, st, ps.global(TL::piece(0, r, w)), ql);
         __builtin_amdgcn_sched_barrier(0);
     }
-    win.fill(a.sktab, -1);
+    win.stage(a.sktab, -1);
     TL::ifft(v, w, lane, lds, ps, win);
     if (!live) return;
 #pragma unroll
@@ -367,7 +425,7 @@ template <class F, int T>
 __global__ void __launch_bounds__(64 << wave_bits(T), 4) k_dec_hi(DecArgs a) {
     using TL = Tile<F, T, reg_bits(T), C>;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    WindowFor<F> win = make_window<F>(lds + tile_lds_dwords<F, T>(), 0, kLoBits, 1u << T);
+    GlobalWindow<F> win;
     const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const uint64_t q0 = lane_units(lane);
     const bool live = q0 < a.nunits;
@@ -379,7 +437,7 @@ __global__ void __launch_bounds__(64 << wave_bits(T), 4) k_dec_hi(DecArgs a) {
         const unsigned tp = TL::piece(0, r, w);
         load_or_zero<F>(v[r], a.a_in, tp < a.nlo, ps.global(tp), a.zeros, ql);
     }
-    win.fill(a.sktab, -1);
+    win.stage(a.sktab, -1);
     TL::ifft(v, w, lane, lds, ps, win);
     TL::copy(d, v);
     TL::derivative_add(d, v, w, lane, lds);
@@ -404,7 +462,7 @@ __global__ void __launch_bounds__(64 << wave_bits(kLoBits), 4) k_dec_fin(DecArgs
         const unsigned L = T, j = blockIdx.y;
         if (!((cload(a.needed_pyr + pyr_offset(L) + (j >> 5)) >> (j & 31)) & 1u)) return;
     }
-    WindowFor<F> win = make_window<F>(lds + tile_lds_dwords<F, T>(), blockIdx.y << T, 0, 1u << T);
+    GlobalWindow<F> win;
     const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const uint64_t q0 = lane_units(lane);
     const bool live = q0 < a.nunits;
@@ -418,7 +476,7 @@ __global__ void __launch_bounds__(64 << wave_bits(kLoBits), 4) k_dec_fin(DecArgs
         load_units<F, C>(z[r], a.a_in.ptr(g), ql);
         load_units<F, C>(v[r], a.b_in.ptr(g), ql);
     }
-    win.fill(a.sktab, -1);
+    win.stage(a.sktab, -1);
     TL::derivative_add(z, v, w, lane, lds);
     TL::fft(z, w, lane, lds, ps, win);
     if (!live) return;
@@ -490,10 +548,10 @@ __global__ void __launch_bounds__(256) k_xor_reduce(XorArgs a) {
     uint4 acc = make_uint4(0, 0, 0, 0);
     for (unsigned i = 0; i < a.count; ++i) {
         const uint8_t* p = a.src.ptr(i);
-        const uint4 v = *reinterpret_cast<const uint4*>(p + q * 4);
+        const uint4 v = *gptr<const uint4>(p + q * 4);
         acc.x ^= v.x; acc.y ^= v.y; acc.z ^= v.z; acc.w ^= v.w;
     }
-    *reinterpret_cast<uint4*>(a.out.ptr(0) + q * 4) = acc;
+    *gptr<uint4>(a.out.ptr(0) + q * 4) = acc;
 }
 
 // ------------------------------------------------------------ dispatching --
@@ -513,8 +571,8 @@ hipError_t launch(KernelFn* fn, dim3 grid, unsigned threads, size_t lds_dwords, 
 }
 
 template <class F, int T>
-constexpr size_t full_tile_lds() {  // transpose area + a window of 2^T entries
-    return tile_lds_dwords<F, T>() + window_dwords<F>(1u << T);
+constexpr size_t full_tile_lds() {  // transpose area + staged skew tables
+    return tile_lds_dwords<F, T>() + SkewTables<F, (64 << wave_bits(T))>::kLdsDwords;
 }
 
 template <class F, int T>
@@ -528,7 +586,7 @@ template <class F, int T>
 struct DecFused8Fn {
     static hipError_t run(const DecArgs& a, hipStream_t s) {
         return launch(&k_dec_fused8<T>, dim3(tiles_for(a.nunits)), 64u << wave_bits(T),
-                      full_tile_lds<FF8, T>() + kLogTab8Dwords, s, &a);
+                      full_tile_lds<FF8, T>() + LdsTab8<257>::kDwords + 256, s, &a);
     }
 };
 template <class F, int T>

@@ -112,6 +112,7 @@ def main():
     device = torch.device("cuda", local)
 
     import leopard_amd as leo
+    from leopard_amd.sharding import max_over_ranks
     assert leo.leo_init() == 0, leo.last_error()
     lib = leo.lib
     stream = torch.cuda.current_stream(device)
@@ -154,11 +155,8 @@ def main():
             raise RuntimeError(leo.last_error())
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    elapsed = t1 - t0
+    elapsed = max_over_ranks(t1 - t0)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
         barrier()
 
     # per-kernel launch durations with HIP events on the launch stream

@@ -265,3 +265,34 @@ def test_baseline_shapes_digest_and_roundtrip(leo, k, r, b):
     idx = torch.tensor(lo, device="cuda")
     stacked = torch.stack([got[i] for i in lo])
     assert torch.equal(stacked, data.index_select(0, idx))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,r,b,world", [(128, 128, 65536, 2), (100, 60, 6400, 3), (300, 100, 64 * 37, 4)])
+def test_column_shards_on_device_equal_whole_call(leo, k, r, b, world):
+    """The multi-GPU path per rank: leo_amd_*_slice over this rank's column
+    range (leopard_amd.sharding), run here for every rank in turn on one
+    device; the union equals one whole-buffer call and the oracle."""
+    import torch
+    from leopard_amd.sharding import decode_shard, encode_shard
+    data = ol.pcg_bytes(11, 2, k, b)
+    o = torch.from_numpy(data).cuda()
+    wc = leo.leo_encode_work_count(k, r)
+    work = torch.zeros((wc, b), dtype=torch.uint8, device="cuda")
+    for rank in range(world):
+        assert encode_shard(b, rank, world, k, r, [o[i].data_ptr() for i in range(k)],
+                            [work[i].data_ptr() for i in range(wc)]) == 0, leo.last_error()
+    torch.cuda.synchronize()
+    rec = work[:r].cpu().numpy()
+    assert np.array_equal(rec, ol.oracle().encode(data, r))
+    lost = list(range(0, min(k, r)))
+    dwc = leo.leo_decode_work_count(k, r)
+    dwork = torch.zeros((dwc, b), dtype=torch.uint8, device="cuda")
+    recd = work[:r].clone()
+    for rank in range(world):
+        assert decode_shard(b, rank, world, k, r, [None if i in lost else o[i].data_ptr() for i in range(k)],
+                            [recd[i].data_ptr() for i in range(r)],
+                            [dwork[i].data_ptr() for i in range(dwc)]) == 0, leo.last_error()
+    torch.cuda.synchronize()
+    for i in lost:
+        assert torch.equal(dwork[i], o[i]), i

@@ -10,7 +10,7 @@ def main():
     dirs = sys.argv[1:] or sorted(glob.glob("gpurun_out/pmc*/"))
     agg = defaultdict(lambda: defaultdict(list))
     for d in dirs:
-        for f in glob.glob(d.rstrip("/") + "/*counter_collection.csv"):
+        for f in glob.glob(d.rstrip("/") + "/**/*counter_collection.csv", recursive=True):
             for row in csv.DictReader(open(f)):
                 name = row["Kernel_Name"]
                 if "lamd" not in name:

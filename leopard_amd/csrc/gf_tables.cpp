@@ -1,6 +1,7 @@
 // gf_tables.cpp -- see gf_tables.h.
 #include "gf_tables.h"
 
+#include <algorithm>
 #include <array>
 
 namespace lamd {
@@ -152,6 +153,21 @@ void build_skew_tables(const GaloisField& f, const std::vector<uint32_t>& perm_t
         }
         const uint32_t* t = &perm_tables[size_t(lm) * tab_dwords];
         for (unsigned d = 0; d < flag_dw; ++d) e[d] = t[d];
+    }
+}
+
+void build_fused_top_tables8(const GaloisField& f, const std::vector<uint32_t>& perm_tables,
+                             std::vector<uint32_t>& out) {
+    out.assign(size_t(kFused8Entries) * kTab8Dwords, 0);
+    auto element = [&](unsigned i) { return f.skew[i] == f.modulus() ? 0u : unsigned(f.exp_of[f.skew[i]]); };
+    for (unsigned T = 1; T <= 7; ++T) {
+        const unsigned m = 1u << T;
+        for (unsigned c = 0; c + 1 < f.order() / m; ++c) {
+            const unsigned e = element(m - 1 + c * m + m / 2) ^ element(m / 2 - 1);
+            if (e == 0) continue;  // multiply by zero: the all-zero table
+            const uint32_t* t = &perm_tables[size_t(f.log_of[e]) * kTab8Dwords];
+            std::copy(t, t + kTab8Dwords, &out[(size_t(T - 1) * 256 + c) * kTab8Dwords]);
+        }
     }
 }
 

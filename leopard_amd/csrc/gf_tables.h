@@ -78,4 +78,11 @@ constexpr unsigned kSkewFlagDw16 = 20;
 void build_skew_tables(const GaloisField& f, const std::vector<uint32_t>& perm_tables, unsigned tab_dwords,
                        unsigned flag_dw, std::vector<uint32_t>& out);
 
+// FF8 encoder: the top IFFT layer of chunk c fused with the top FFT layer
+// (rs_ff8.hip): entry (T - 1) * 256 + c holds the multiply table (kTab8Dwords)
+// of skew-element(m - 1 + c*m + m/2) + skew-element(m/2 - 1), m = 2^T.
+constexpr unsigned kFused8Entries = 7 * 256;
+void build_fused_top_tables8(const GaloisField& f, const std::vector<uint32_t>& perm_tables,
+                             std::vector<uint32_t>& out);
+
 }  // namespace lamd

@@ -55,6 +55,7 @@ struct DeviceTables {
     uint32_t* tab16 = nullptr;  // (65536 + 1) x 24 dwords
     uint32_t* sktab8 = nullptr;   // skew-indexed butterfly tables, 256 x 8 dwords
     uint32_t* sktab16 = nullptr;  // 65536 x 24 dwords
+    uint32_t* fused8 = nullptr;  // fused top-layer tables of the FF8 encoder
     uint32_t* walsh8 = nullptr;
     uint32_t* walsh16 = nullptr;
     uint8_t* zeros = nullptr;   // zero page
@@ -65,7 +66,7 @@ std::mutex g_mu;
 bool g_initialized = false;
 int g_device_count = 0;
 std::vector<DeviceTables> g_dev;
-std::vector<uint32_t> g_h_tab8, g_h_tab16, g_h_sktab8, g_h_sktab16, g_h_walsh8, g_h_walsh16;
+std::vector<uint32_t> g_h_tab8, g_h_tab16, g_h_sktab8, g_h_sktab16, g_h_fused8, g_h_walsh8, g_h_walsh16;
 
 template <class T>
 hipError_t upload(T** dst, const std::vector<T>& src) {
@@ -86,6 +87,7 @@ LeopardResult ensure_device(int dev, DeviceTables** out) {
         HIP_OK(upload(&d.tab16, g_h_tab16), "upload FF16 tables");
         HIP_OK(upload(&d.sktab8, g_h_sktab8), "upload FF8 skew tables");
         HIP_OK(upload(&d.sktab16, g_h_sktab16), "upload FF16 skew tables");
+        HIP_OK(upload(&d.fused8, g_h_fused8), "upload FF8 fused tables");
         HIP_OK(upload(&d.walsh8, g_h_walsh8), "upload FF8 LogWalsh");
         HIP_OK(upload(&d.walsh16, g_h_walsh16), "upload FF16 LogWalsh");
         HIP_OK(hipMalloc(reinterpret_cast<void**>(&d.zeros), 4096), "zero page");
@@ -277,6 +279,21 @@ LeopardResult encode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
     const unsigned Tm = log2u(m);
     const unsigned nchunks = (K + m - 1) / m;
 
+    if (!ff16) {  // n <= 256: one fused kernel, launch data by value (rs_ff8.hip)
+        Ff8EncArgs a;
+        std::memset(&a, 0, sizeof(a));
+        for (unsigned i = 0; i < K; ++i) a.ptr[i] = uint64_t(reinterpret_cast<uintptr_t>(orig[i])) + off;
+        for (unsigned i = 0; i < R; ++i) a.ptr[K + i] = uint64_t(reinterpret_cast<uintptr_t>(work[i])) + off;
+        a.sktab = c.t->sktab8;
+        a.fused = c.t->fused8 + size_t(Tm - 1) * 256 * kTab8Dwords;
+        a.K = K;
+        a.R = R;
+        a.nchunks = nchunks;
+        a.nunits = uint32_t(bytes / 4);
+        HIP_OK(launch_ff8_encode(Tm, a, c.s), "encode kernel");
+        return Leopard_Success;
+    }
+
     EncArgs a;
     std::memset(&a, 0, sizeof(a));
     MapBuilder mb;
@@ -306,7 +323,7 @@ LeopardResult encode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
 
     if (!multipass) {
         a.nunits = bytes / unit_bytes;
-        HIP_OK(launch_encode_fused(ff16, Tm, a, c.s), "encode kernel");
+        HIP_OK(launch_encode_fused16(Tm, a, c.s), "encode kernel");
         return Leopard_Success;
     }
     uint8_t* U = c.ws->dbuf + table_bytes;
@@ -348,27 +365,70 @@ LeopardResult xor_device(Call& c, uint64_t bytes, uint64_t off, const void* cons
 
 // --------------------------------------------------------------- decode ----
 
+// FF8 error locator on the host (n <= 256 positions, a few thousand integer ops):
+// el = FWHT(LogWalsh * FWHT(erasures)) mod 255 (LeopardFF8.cpp:1848-1853).  The
+// last pattern is cached per thread (repeated erasure patterns are common).
+void error_locator8(const std::vector<uint32_t>& erased, uint32_t* el_bytes) {
+    thread_local uint32_t last_pattern[8] = {~0u, 0, 0, 0, 0, 0, 0, 0};
+    thread_local uint32_t last_el[kFf8Ptrs / 4];
+    if (std::memcmp(last_pattern, erased.data(), sizeof(last_pattern)) != 0) {
+        const GaloisField& f = field8();
+        uint16_t e[256];
+        for (unsigned p = 0; p < 256; ++p) e[p] = (erased[p >> 5] >> (p & 31)) & 1u;
+        f.walsh(e, 256);
+        for (unsigned p = 0; p < 256; ++p) e[p] = uint16_t((unsigned(e[p]) * f.log_walsh[p]) % 255u);
+        f.walsh(e, 256);
+        for (unsigned q = 0; q < 64; ++q)
+            last_el[q] = uint32_t(e[4 * q] % 255u) | uint32_t(e[4 * q + 1] % 255u) << 8 |
+                         uint32_t(e[4 * q + 2] % 255u) << 16 | uint32_t(e[4 * q + 3] % 255u) << 24;
+        std::memcpy(last_pattern, erased.data(), sizeof(last_pattern));
+    }
+    std::memcpy(el_bytes, last_el, sizeof(last_el));
+}
+
+LeopardResult decode_device8(Call& c, uint64_t bytes, uint64_t off, unsigned K, unsigned R, unsigned m, unsigned Tn,
+                             const void* const* orig, const void* const* rec, void** work,
+                             const std::vector<uint32_t>& erased) {
+    Ff8DecArgs a;
+    std::memset(&a, 0, sizeof(a));
+    auto mark = [](uint32_t* pyr, unsigned p) {
+        for (unsigned L = 0; L <= 8; ++L) {
+            const unsigned j = p >> L;
+            pyr[pyr8_offset(L) + (j >> 5)] |= 1u << (j & 31);
+        }
+    };
+    auto addr = [&](const void* p) { return uint64_t(reinterpret_cast<uintptr_t>(p)) + off; };
+    for (unsigned i = 0; i < R; ++i)
+        if (rec[i]) {
+            a.ptr[i] = addr(rec[i]);
+            mark(a.present, i);
+        }
+    for (unsigned i = 0; i < K; ++i) {
+        if (orig[i]) {
+            a.ptr[m + i] = addr(orig[i]);
+            mark(a.present, m + i);
+        } else {
+            a.ptr[m + i] = addr(work[i]);  // lost: its slot carries the output
+            mark(a.needed, m + i);
+        }
+    }
+    error_locator8(erased, a.el);
+    a.sktab = c.t->sktab8;
+    a.tabs = c.t->tab8;
+    a.K = K;
+    a.R = R;
+    a.m = m;
+    a.nunits = uint32_t(bytes / 4);
+    HIP_OK(launch_ff8_decode(Tn, a, c.s), "decode kernel");
+    return Leopard_Success;
+}
+
 LeopardResult decode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, unsigned R, const void* const* orig,
                             const void* const* rec, void** work) {
     const unsigned m = next_pow2(R);
     const unsigned n = next_pow2(m + K);
     const bool ff16 = n > 256;
     const unsigned Tn = log2u(n);
-
-    DecArgs a;
-    std::memset(&a, 0, sizeof(a));
-    MapBuilder mb;
-    mb.build(a.orig, orig, K, off);
-    mb.build(a.rec, rec, R, off);
-    mb.build(a.out, work, K, off);
-    a.sktab = ff16 ? c.t->sktab16 : c.t->sktab8;
-    a.tabs = ff16 ? c.t->tab16 : c.t->tab8;
-    a.zeros = c.t->zeros;
-    a.walsh = ff16 ? c.t->walsh16 : c.t->walsh8;
-    a.K = K;
-    a.R = R;
-    a.m = m;
-    a.Tn = Tn;
 
     // error_locations[] = 1 at lost recoveries, [R, m), lost originals (LeopardFF8.cpp:1825-1840)
     std::vector<uint32_t> erased((std::max(n, 256u) + 31) / 32, 0);
@@ -379,17 +439,22 @@ LeopardResult decode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
     for (unsigned i = 0; i < K; ++i)
         if (!orig[i]) set(m + i);
 
-    if (!ff16) {
-        std::memcpy(a.erased8, erased.data(), sizeof(a.erased8));
-        const size_t table_bytes = (mb.bytes() + 255) / 256 * 256;
-        LeopardResult r = c.ws->reserve_device(table_bytes);
-        if (r != Leopard_Success) return r;
-        r = mb.flush(*c.ws, reinterpret_cast<uint64_t*>(c.ws->dbuf), c.s);
-        if (r != Leopard_Success) return r;
-        a.nunits = bytes / 4;
-        HIP_OK(launch_decode_fused8(Tn, a, c.s), "decode kernel");
-        return Leopard_Success;
-    }
+    if (!ff16) return decode_device8(c, bytes, off, K, R, m, Tn, orig, rec, work, erased);
+
+    DecArgs a;
+    std::memset(&a, 0, sizeof(a));
+    MapBuilder mb;
+    mb.build(a.orig, orig, K, off);
+    mb.build(a.rec, rec, R, off);
+    mb.build(a.out, work, K, off);
+    a.sktab = c.t->sktab16;
+    a.tabs = c.t->tab16;
+    a.zeros = c.t->zeros;
+    a.walsh = c.t->walsh16;
+    a.K = K;
+    a.R = R;
+    a.m = m;
+    a.Tn = Tn;
 
     // FF16: erasure bitmap (full 65536 positions) + error locator on the device,
     // plus occupancy pyramids for pruning (received data / lost originals).
@@ -737,6 +802,7 @@ LEO_EXPORT int leo_init_(int version) {
     build_perm_tables16(f16, g_h_tab16);
     build_skew_tables(f8, g_h_tab8, kTab8Dwords, kSkewFlagDw8, g_h_sktab8);
     build_skew_tables(f16, g_h_tab16, kTab16Dwords, kSkewFlagDw16, g_h_sktab16);
+    build_fused_top_tables8(f8, g_h_tab8, g_h_fused8);
     g_h_walsh8.assign(f8.log_walsh.begin(), f8.log_walsh.end());
     g_h_walsh16.assign(f16.log_walsh.begin(), f16.log_walsh.end());
     g_dev.assign(count, DeviceTables{});

@@ -35,14 +35,35 @@ struct DecArgs {
     const uint32_t* sktab;
     const uint32_t* tabs;
     const uint8_t* zeros;
-    const uint32_t* walsh;
+    const uint32_t* walsh;  // FF16 LogWalsh
     const uint32_t* present_pyr;  // FF16: "any received data" pyramid over positions
-    const uint32_t* needed_pyr;   // FF16: "any lost original" pyramid over positions       // FF8: LogWalsh for the in-kernel error locator
+    const uint32_t* needed_pyr;   // FF16: "any lost original" pyramid over positions
     const uint32_t* el;          // FF16: precomputed error locator logs
     const uint32_t* erased_dev;  // FF16: erasure bitmap over positions [0, n)
-    uint32_t erased8[8];         // FF8: erasure bitmap by value
     unsigned K, R, m, Tn, nlo;   // nlo: number of non-zero low tiles
     uint64_t nunits;
+};
+
+// GF(2^8) kernels (codeword length n <= 256).  Everything a launch needs travels
+// by value in the kernel arguments (< 4 KiB), so a wave's prologue is one batch
+// of scalar loads with no pointer-chasing or branching on piece maps.
+constexpr unsigned kFf8Ptrs = 256;
+struct Ff8EncArgs {
+    uint64_t ptr[kFf8Ptrs];  // [0, K) originals, [K, K + R) recovery outputs (launch's column base applied)
+    const uint32_t* sktab;   // skew-indexed butterfly tables, 8 dwords per entry
+    const uint32_t* fused;   // fused top-layer tables of this m, entry c for chunk c (8 dwords)
+    unsigned K, R, nchunks;
+    uint32_t nunits;         // dword columns per piece in this launch
+};
+struct Ff8DecArgs {
+    uint64_t ptr[kFf8Ptrs];        // position p: received piece / output of a lost original / 0
+    uint32_t present[kPyr8Words];  // pyramid of received positions (Pyr8Live)
+    uint32_t needed[kPyr8Words];   // pyramid of lost originals
+    uint32_t el[kFf8Ptrs / 4];     // error locator logs (host computed), one byte per position
+    const uint32_t* sktab;
+    const uint32_t* tabs;          // multiply tables by log value; entry 256 is all zero
+    unsigned K, R, m;
+    uint32_t nunits;
 };
 
 struct XorArgs {
@@ -53,17 +74,18 @@ struct XorArgs {
 };
 
 // Launchers (rs_kernels.hip).  Return hipSuccess or the launch error.
-hipError_t launch_encode_fused(int ff16, unsigned T, const EncArgs& a, hipStream_t s);
+hipError_t launch_encode_fused16(unsigned T, const EncArgs& a, hipStream_t s);
 hipError_t launch_encode_lo(const EncArgs& a, hipStream_t s);
 hipError_t launch_encode_hi(const EncArgs& a, hipStream_t s);
 hipError_t launch_encode_fin(const EncArgs& a, hipStream_t s);
-hipError_t launch_decode_fused8(unsigned T, const DecArgs& a, hipStream_t s);
 hipError_t launch_decode_lo(const DecArgs& a, hipStream_t s);
 hipError_t launch_decode_hi(const DecArgs& a, hipStream_t s);
 hipError_t launch_decode_fin(const DecArgs& a, hipStream_t s);
 hipError_t launch_error_locator16(const uint32_t* erased, const uint32_t* walsh, uint32_t* tmp, uint32_t* el,
                                   hipStream_t s);
 hipError_t launch_xor_reduce(const XorArgs& a, hipStream_t s);
+hipError_t launch_ff8_encode(unsigned T, const Ff8EncArgs& a, hipStream_t s);
+hipError_t launch_ff8_decode(unsigned T, const Ff8DecArgs& a, hipStream_t s);
 
 // Units per lane chosen for each kernel family (the host sizes grids with it).
 constexpr int kUnitsPerLane = 1;

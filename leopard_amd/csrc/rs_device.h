@@ -28,7 +28,9 @@
 // Ablation switches for performance experiments only (tools/ablate.sh builds
 // separate libraries with them; the shipped library has LAMD_ABLATE == 0):
 // 1 = no butterfly arithmetic, 2 = no LDS transposes, 4 = no piece loads,
-// 8 = no piece stores, 16 = fused kernels return at once (launch floor).
+// 8 = no piece stores, 16 = fused kernels return at once (launch floor),
+// 32 = FF8 decoder: no in-kernel error locator, 64 = no formal derivative,
+// 128 = FF8 decoder: no scale / reveal multiplies, 256 = no table staging.
 #ifndef LAMD_ABLATE
 #define LAMD_ABLATE 0
 #endif
@@ -300,6 +302,7 @@ struct TabStage8 {
     uint4 va[PER];
     uint32_t vc[PER];
     LDEV void load(const uint32_t* src) {
+        if constexpr ((LAMD_ABLATE & 256) != 0) return;
         static_for<0, int(PER)>([&](auto I) __attribute__((always_inline)) {
             constexpr unsigned i = decltype(I)::value;
             unsigned e = threadIdx.x + i * NT;
@@ -311,6 +314,7 @@ struct TabStage8 {
     template <unsigned M>
     LDEV void store(LdsTab8<M> dst) const {
         static_assert(M >= N, "destination too small");
+        if constexpr ((LAMD_ABLATE & 256) != 0) return;
         static_for<0, int(PER)>([&](auto I) __attribute__((always_inline)) {
             constexpr unsigned i = decltype(I)::value;
             const unsigned e = threadIdx.x + i * NT;
@@ -326,6 +330,35 @@ struct TabStage8 {
 struct PieceSpace {
     unsigned lo_fixed, l0, hi_fixed;
     LDEV unsigned global(unsigned tp) const { return lo_fixed | (tp << l0) | hi_fixed; }
+};
+
+// Pruning predicates.  A butterfly layer on global bit l acts inside aligned
+// blocks of 2^(l+1) codeword positions; pred(pos, l + 1) says whether the
+// block holding position pos is live.  IFFT: a block with no non-zero input
+// stays all-zero, so its butterflies are skipped; FFT: a block holding no
+// needed output feeds no needed output, so its butterflies are skipped (the
+// reference's FFT_DIT_ErrorBits, LeopardFF8.cpp:1681-1801, generalised to both
+// transforms).  Every predicate is wave-uniform (scalar).
+struct AllLive {
+    LDEV constexpr bool operator()(unsigned, unsigned) const { return true; }
+};
+// Live iff the block starts below `limit` (encoder: inputs [0, K - base),
+// outputs [0, R)).
+struct BelowLive {
+    unsigned limit;
+    LDEV bool operator()(unsigned pos, unsigned level) const { return ((pos >> level) << level) < limit; }
+};
+// Occupancy pyramid: level L holds one bit per aligned block of 2^L positions,
+// starting at word off(L).  FF8: 256 positions, 20 words, passed by value in
+// the kernel arguments.  FF16: 65536 positions in device memory (pyr_offset).
+constexpr unsigned pyr8_offset(unsigned L) { return L <= 3 ? 16u - (16u >> L) : 15u + (L - 4); }
+constexpr unsigned kPyr8Words = 20;
+struct Pyr8Live {
+    const uint32_t* w;  // kernel-argument words
+    LDEV bool operator()(unsigned pos, unsigned level) const {
+        const unsigned j = pos >> level;
+        return (w[pyr8_offset(level) + (j >> 5)] >> (j & 31)) & 1u;
+    }
 };
 
 // Skew index of the butterfly on pair (i, i + 2^l), bit l of i clear: the
@@ -392,13 +425,14 @@ struct Tile {
     //   IFFT (LeopardFF8.cpp:595-666):  y ^= x; x ^= y * skew   (skipped if skew is 0)
     //   FFT  (LeopardFF8.cpp:1319-1390): x ^= y * skew; y ^= x
     // win holds the stage's butterfly tables (skew base already applied).
-    template <bool kInverse, int LAY, int L, class Win>
-    LDEV static void layer(Reg& x, unsigned w, const PieceSpace& ps, const Win& win) {
+    template <bool kInverse, int LAY, int L, class Win, class Pred>
+    LDEV static void layer(Reg& x, unsigned w, const PieceSpace& ps, const Win& win, const Pred& pred) {
         if constexpr ((LAMD_ABLATE & 1) != 0) return;
         constexpr int rb = L - lo(LAY);
         static_assert(rb >= 0 && rb < R, "layer not in this layout");
         constexpr int half = 1 << rb;
         const unsigned gl = ps.l0 + L;
+        auto live = [&](int g) { return pred(ps.global(piece(LAY, g, w)), gl + 1); };
         auto table = [&](int g) {
             // A zero skew has an all-zero table: the multiply-add adds 0, which is
             // the reference's XOR-only butterfly without a branch (branches around
@@ -415,7 +449,13 @@ struct Tile {
                     uint32_t* b = &x[g + j + half][u * F::kDw];
                     if constexpr (kInverse) {
 #pragma unroll
-                        for (int k = 0; k < F::kDw; ++k) b[k] ^= a[k];
+                        for (int k = 0; k < F::kDw; ++k) {
+                            b[k] ^= a[k];
+                            // Materialise y: otherwise the compiler folds (y ^ x) & mask
+                            // into one v_bitop3 (VOP3, ~1.6x the issue cost of the
+                            // VOP2 and it replaces; measured 12% per butterfly).
+                            if constexpr (F::kDw == 1) asm volatile("" : "+v"(b[k]));
+                        }
                         F::muladd(a, b, t);
                     } else {
                         F::muladd(a, b, t);
@@ -437,7 +477,10 @@ struct Tile {
                 // keep earlier reads of the same entries live across the transform.
                 asm volatile("" ::: "memory");
                 static_for<0, KB>([&](auto GI) { tabs[GI.value] = table((g0 + GI.value) * 2 * half); });
-                static_for<0, KB>([&](auto GI) { group((g0 + GI.value) * 2 * half, tabs[GI.value]); });
+                static_for<0, KB>([&](auto GI) {
+                    constexpr int g = (g0 + GI.value) * 2 * half;
+                    if (live(g)) group(g, tabs[GI.value]);
+                });
                 __builtin_amdgcn_sched_barrier(0);  // keep the next batch's tables below this one
             });
         } else {
@@ -448,9 +491,37 @@ struct Tile {
                 const typename F::Tab t = next;
                 if constexpr (g + 2 * half < NR) next = table(g + 2 * half);
                 __builtin_amdgcn_sched_barrier(0);
-                group(g, t);
+                if (live(g)) group(g, t);
                 __builtin_amdgcn_sched_barrier(0);
             });
+        }
+    }
+
+    // The top IFFT layer of one stage followed by the top FFT layer of the next,
+    // on the same pairs (i, i + 2^(T-1)), as one butterfly (layout kLast):
+    //   IFFT  y1 = y ^ x, x1 = x ^ c1*y1;  FFT  x2 = x1 ^ c2*y1, y2 = y1 ^ x2
+    //   =>    y1 = y ^ x, x2 = x ^ (c1 + c2)*y1, y2 = y1 ^ x2
+    // t is the multiply table of the field element c1 + c2 (one group: the top
+    // layer has a single skew).  Saves one multiply layer per encode.
+    LDEV static void fused_top(Reg& x, const typename F::Tab& t) {
+        if constexpr ((LAMD_ABLATE & 1) != 0) return;
+        constexpr int half = 1 << (T - 1 - lo(kLast));
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            if (r & half) continue;
+#pragma unroll
+            for (int u = 0; u < C; ++u) {
+                uint32_t* a = &x[r][u * F::kDw];
+                uint32_t* b = &x[r + half][u * F::kDw];
+#pragma unroll
+                for (int k = 0; k < F::kDw; ++k) {
+                    b[k] ^= a[k];
+                    if constexpr (F::kDw == 1) asm volatile("" : "+v"(b[k]));
+                }
+                F::muladd(a, b, t);
+#pragma unroll
+                for (int k = 0; k < F::kDw; ++k) b[k] ^= a[k];
+            }
         }
     }
 
@@ -475,23 +546,29 @@ struct Tile {
     }
 
     // IFFT over all tile bits: starts in layout 0, ends in layout kLast.
-    template <class Win>
-    LDEV static void ifft(Reg& x, unsigned w, unsigned lane, uint32_t* lds, const PieceSpace& ps, const Win& win) {
+    // kSkipTop: leave out the layer on the top tile bit (fused_top does it).
+    template <bool kSkipTop = false, class Win, class Pred = AllLive>
+    LDEV static void ifft(Reg& x, unsigned w, unsigned lane, uint32_t* lds, const PieceSpace& ps, const Win& win,
+                          const Pred& pred = Pred{}) {
         static_for<0, NL>([&](auto K) {
             constexpr int k = decltype(K)::value;
-            static_for<ifft_begin(k), lo(k) + R>([&](auto L) { layer<true, k, decltype(L)::value>(x, w, ps, win); });
+            constexpr int end = (kSkipTop && k == NL - 1) ? T - 1 : lo(k) + R;
+            static_for<ifft_begin(k), end>(
+                [&](auto L) { layer<true, k, decltype(L)::value>(x, w, ps, win, pred); });
             if constexpr (k + 1 < NL) transpose<k, k + 1>(x, w, lane, lds);
         });
     }
 
     // FFT over all tile bits: starts in layout kLast, ends in layout 0.
-    template <class Win>
-    LDEV static void fft(Reg& x, unsigned w, unsigned lane, uint32_t* lds, const PieceSpace& ps, const Win& win) {
+    template <bool kSkipTop = false, class Win, class Pred = AllLive>
+    LDEV static void fft(Reg& x, unsigned w, unsigned lane, uint32_t* lds, const PieceSpace& ps, const Win& win,
+                         const Pred& pred = Pred{}) {
         static_for<0, NL>([&](auto KI) {
             constexpr int k = NL - 1 - decltype(KI)::value;
-            static_for<lo(k), fft_end(k)>([&](auto LI) {
-                constexpr int L = fft_end(k) - 1 - (decltype(LI)::value - lo(k));
-                layer<false, k, L>(x, w, ps, win);
+            constexpr int end = (kSkipTop && k == NL - 1) ? T - 1 : fft_end(k);
+            static_for<lo(k), end>([&](auto LI) {
+                constexpr int L = end - 1 - (decltype(LI)::value - lo(k));
+                layer<false, k, L>(x, w, ps, win, pred);
             });
             if constexpr (k > 0) transpose<k, k - 1>(x, w, lane, lds);
         });
@@ -501,6 +578,7 @@ struct Tile {
     // (layout kLast).  Register bits: ascending r reads v[r | 2^b] before it is
     // modified; wave bits: gathered from an LDS copy of the original v.
     LDEV static void derivative_inplace(Reg& v, unsigned w, unsigned lane, uint32_t* lds) {
+        if constexpr ((LAMD_ABLATE & 64) != 0) return;
         if constexpr (T > R) {
             __syncthreads();
 #pragma unroll

@@ -9,8 +9,8 @@
 //   lost original i = FFT_n(z)[m + i] * exp(-el[m + i])
 //
 // Kernel families (T = tile bits, see rs_device.h):
-//   k_enc_fused / k_dec_fused : the whole transform in one workgroup tile
-//                               (FF8: m <= 128, n <= 256; FF16 encode m <= 256)
+//   k_enc_fused<FF16>         : the whole encode transform in one workgroup tile (m <= 256)
+//   (GF(2^8), n <= 256, lives in rs_ff8.hip)
 //   k_enc_lo/hi/fin, k_dec_lo/hi/fin : FF16 transforms of 2^9 .. 2^16 pieces as
 //     three tile passes: low 8 bits, high bits, low 8 bits again.  The formal
 //     derivative is split between the passes with
@@ -30,18 +30,20 @@ constexpr int C = kUnitsPerLane;
 // Register bits per lane for a tile of T bits: 8 pieces per lane when that
 // gives at most 16 waves (more waves per SIMD hide the butterfly chains'
 // latency), otherwise 16 pieces (T = 8: 16 waves of 16 pieces).
-constexpr int reg_bits(int T) { return T <= 3 ? T : (T - 3 <= 4 ? 3 : T - 4); }
+#ifndef LAMD_RB7  // experiment hook: register bits for 7-bit tiles
+#define LAMD_RB7 3
+#endif
+constexpr int reg_bits(int T) { return T <= 3 ? T : T == 7 ? LAMD_RB7 : (T - 3 <= 4 ? 3 : T - 4); }
 constexpr int wave_bits(int T) { return T - reg_bits(T); }
 
-// LDS carve-up: [tile transpose area][FF8: skew tables][FF8 decoder: log tables, error locator]
+// LDS carve-up: the tile transpose area
 template <class F, int T>
 constexpr size_t tile_lds_dwords() {
     return wave_bits(T) > 0 ? (size_t(1) << T) * 64 * C * F::kDw : 0;  // transposes
 }
 
-// Butterfly tables of a kernel: FF16 reads them through the scalar cache; FF8
-// stages the whole skew-indexed array into LDS once (TabStage8: global loads
-// issued before the piece loads, LDS stores + the one barrier after them).
+// Butterfly tables of a kernel: FF16 reads them through the scalar cache (the
+// FF8 kernels in rs_ff8.hip stage theirs in LDS).
 template <class F, int NT>
 struct SkewTables {
     using Win = GlobalWindow<F>;
@@ -50,16 +52,6 @@ struct SkewTables {
     LDEV void publish(uint32_t*) const {}
     LDEV static Win window(uint32_t*) { return Win{}; }
 };
-template <int NT>
-struct SkewTables<FF8, NT> {
-    using Win = LdsSkew8;
-    static constexpr size_t kLdsDwords = LdsTab8<256>::kDwords;
-    TabStage8<NT, 256> st;
-    LDEV void load(const uint32_t* sktab) { st.load(sktab); }
-    LDEV void publish(uint32_t* lds) const { st.store(LdsTab8<256>{lds}); }
-    LDEV static Win window(uint32_t* lds) { return Win{LdsTab8<256>{lds}}; }
-};
-
 LDEV uint64_t lane_units(unsigned lane) { return (uint64_t(blockIdx.x) * 64 + lane) * C; }
 
 // Piece i of pm when `ok` (wave-uniform), else zeros read from the zero page.
@@ -106,13 +98,13 @@ __global__ void __launch_bounds__(64 << wave_bits(T), 4) k_enc_fused(EncArgs a) 
     TL::zero(acc);
     for (unsigned c = 0;;) {
         win.stage(a.sktab, int(m - 1 + c * m));
-        TL::ifft(x, w, lane, lds, ps, win);
+        TL::ifft(x, w, lane, lds, ps, win, BelowLive{a.K - c * m});
         TL::xor_into(acc, x);
         if (++c >= a.nchunks) break;
         load_chunk(c);
     }
     win.stage(a.sktab, -1);
-    TL::fft(acc, w, lane, lds, ps, win);
+    TL::fft(acc, w, lane, lds, ps, win, BelowLive{a.R});
     TL::pin(acc);
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) {
@@ -142,7 +134,7 @@ __global__ void __launch_bounds__(64 << wave_bits(kLoBits), 4) k_enc_lo(EncArgs 
         load_or_zero<F>(x[r], a.in, base + g < a.K, base + g, a.zeros, ql);
     }
     win.stage(a.sktab, int(m - 1 + base));
-    TL::ifft(x, w, lane, lds, ps, win);
+    TL::ifft(x, w, lane, lds, ps, win, BelowLive{a.K - base});
     if (!live) return;
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) {
@@ -174,12 +166,12 @@ __global__ void __launch_bounds__(64 << wave_bits(T), 4) k_enc_hi(EncArgs a) {
             load_or_zero<F>(x[r], a.slab_in, base + (tp << kLoBits) < a.K, base + ps.global(tp), a.zeros, ql);
         }
         win.stage(a.sktab, int(m - 1 + base));
-        TL::ifft(x, w, lane, lds, ps, win);
+        TL::ifft(x, w, lane, lds, ps, win, BelowLive{a.K - base});
         if (c == 0) TL::copy(acc, x);
         else TL::xor_into(acc, x);
     }
     win.stage(a.sktab, -1);
-    TL::fft(acc, w, lane, lds, ps, win);
+    TL::fft(acc, w, lane, lds, ps, win, BelowLive{a.R});
     if (!live) return;
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) {
@@ -204,7 +196,7 @@ __global__ void __launch_bounds__(64 << wave_bits(kLoBits), 4) k_enc_fin(EncArgs
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) load_units<F, C>(x[r], a.slab_in.ptr(ps.global(TL::piece(TL::kLast, r, w))), ql);
     win.stage(a.sktab, -1);
-    TL::fft(x, w, lane, lds, ps, win);
+    TL::fft(x, w, lane, lds, ps, win, BelowLive{a.R});
     if (!live) return;
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) {
@@ -217,6 +209,16 @@ __global__ void __launch_bounds__(64 << wave_bits(kLoBits), 4) k_enc_fin(EncArgs
 
 LDEV bool bit_set(const uint32_t* bits, unsigned p) { return (cload(bits + (p >> 5)) >> (p & 31)) & 1u; }
 
+// FF16 occupancy pyramid in device memory (rs_args.h: pyr_offset), read through
+// the scalar cache; see rs_device.h for the pruning rule.
+struct Pyr16Live {
+    const uint32_t* pyr;
+    LDEV bool operator()(unsigned pos, unsigned level) const {
+        const unsigned j = pos >> level;
+        return (cload(pyr + pyr_offset(level) + (j >> 5)) >> (j & 31)) & 1u;
+    }
+};
+
 // FF16 decoder state in device memory: erasure bitmap (bit p <=>
 // error_locations[p] = 1, LeopardFF8.cpp:1825-1840) and error locator logs.
 // Multiply tables by log value come through the scalar cache.
@@ -228,65 +230,6 @@ struct State16 {
     LDEV unsigned loc(unsigned p) const { return cload(el + p); }
     LDEV FF16::Tab table(unsigned lm) const { return FF16::tab(tabs, lm); }
 };
-
-// FF8 error locator (LeopardFF8.cpp:1848-1853), computed inside the decode
-// kernel by wave 0 while the piece loads of all waves are in flight:
-// el = FWHT(LogWalsh * FWHT(erasures)) mod 255 for the 256 positions, lane
-// holding positions lane + 64 j, written to LDS.
-//
-// The transforms run on plain signed integers and reduce once at the end:
-// every step is congruent mod 255 to the reference's mod-255 butterflies
-// (|values| stay below 2^25).  Results are fully reduced (0..254), congruent
-// to the reference's partially reduced ones; the multiply tables treat log 0
-// and log 255 identically.  Cross-lane partners come from DPP (lane ^ 1..8)
-// and the gfx950 permlane swaps (lane ^ 16, 32): VALU only, no LDS round trip.
-struct El8 {
-    template <int D>
-    LDEV static int partner(int v, unsigned lane) {
-        if constexpr (D == 1) return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
-        else if constexpr (D == 2) return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);  // [2,3,0,1]
-        else if constexpr (D == 4)  // quad_perm [3,2,1,0] (^3), then row_half_mirror (^7)
-            return __builtin_amdgcn_mov_dpp(__builtin_amdgcn_mov_dpp(v, 0x1B, 0xF, 0xF, false), 0x141, 0xF, 0xF, false);
-        else if constexpr (D == 8)  // row_mirror (^15), then row_half_mirror (^7)
-            return __builtin_amdgcn_mov_dpp(__builtin_amdgcn_mov_dpp(v, 0x140, 0xF, 0xF, false), 0x141, 0xF, 0xF, false);
-        else if constexpr (D == 16) {
-            const auto r = __builtin_amdgcn_permlane16_swap(unsigned(v), unsigned(v), false, false);
-            return int((lane & 16u) ? r[0] : r[1]);
-        } else {
-            const auto r = __builtin_amdgcn_permlane32_swap(unsigned(v), unsigned(v), false, false);
-            return int((lane & 32u) ? r[0] : r[1]);
-        }
-    }
-    // (a, b) -> (a + b, a - b) on every pair of positions differing in one bit
-    LDEV static void fwht(int (&e)[4], unsigned lane) {
-        static_for<0, 6>([&](auto I) {
-            constexpr int D = 1 << decltype(I)::value;
-            int o[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) o[j] = partner<D>(e[j], lane);
-            const bool upper = (lane & unsigned(D)) != 0;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) e[j] = upper ? o[j] - e[j] : e[j] + o[j];
-        });
-        const int a0 = e[0] + e[1], a1 = e[0] - e[1], a2 = e[2] + e[3], a3 = e[2] - e[3];
-        e[0] = a0 + a2; e[2] = a0 - a2;
-        e[1] = a1 + a3; e[3] = a1 - a3;
-    }
-    LDEV static void compute(const DecArgs& a, const unsigned (&walsh)[4], unsigned lane, uint32_t* el_lds) {
-        int e[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) e[j] = int((a.erased8[2 * j + (lane >> 5)] >> (lane & 31)) & 1u);
-        fwht(e, lane);  // |e| <= 256
-#pragma unroll
-        for (int j = 0; j < 4; ++j) e[j] = int((unsigned(e[j] + 510) % 255u) * walsh[j]);  // < 2^16
-        fwht(e, lane);  // |e| < 2^24
-#pragma unroll
-        for (int j = 0; j < 4; ++j) el_lds[lane + 64 * j] = unsigned(e[j] + 255 * 65536) % 255u;
-    }
-};
-
-// Erasure bit of codeword position p (wave-uniform) from the by-value bitmap.
-LDEV bool erased8(const DecArgs& a, unsigned p) { return (a.erased8[p >> 5] >> (p & 31)) & 1u; }
 
 // Received piece at codeword position p, scaled by exp(el[p]); zero if absent.
 // Positions: [0, m) recovery (only [0, R) exist), [m, m+K) originals
@@ -320,80 +263,6 @@ LDEV void reveal(const uint32_t* z, const DecArgs& a, const St& st, unsigned p, 
     }
 }
 
-// Whole FF8 decode in one tile (n <= 256):
-//   prologue: table loads (global) -> piece loads -> tables to LDS, wave 0
-//             computes the error locator into LDS -> one barrier;
-//   scale received pieces by exp(el) (LeopardFF8.cpp:1857-1877), IFFT,
-//   formal derivative (closed form), FFT, reveal lost originals * exp(-el).
-template <int T>
-__global__ void __launch_bounds__(64 << wave_bits(T), 4) k_dec_fused8(DecArgs a) {
-    if constexpr ((LAMD_ABLATE & 16) != 0) return;
-    using F = FF8;
-    using TL = Tile<F, T, reg_bits(T), C>;
-    constexpr int NT = 64 << wave_bits(T);
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    const LdsTab8<256> sk_tabs{lds + tile_lds_dwords<F, T>()};
-    const LdsTab8<257> ltab{sk_tabs.base + LdsTab8<256>::kDwords};  // by log value, 256 = zero
-    uint32_t* el = ltab.base + LdsTab8<257>::kDwords;
-    const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    TabStage8<NT, 256> sk_stage;
-    TabStage8<NT, 256> log_stage;  // entry 256 (the zero table) is written directly
-    sk_stage.load(a.sktab);
-    log_stage.load(a.tabs);
-    unsigned walsh[4] = {0, 0, 0, 0};
-    if (w == 0)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) walsh[j] = a.walsh[lane + 64 * j];
-    const uint64_t q0 = lane_units(lane);
-    const bool live = q0 < a.nunits;
-    const uint64_t ql = live ? q0 : a.nunits - C;
-    const PieceSpace ps{0, 0, 0};
-    LdsSkew8 win{sk_tabs};
-
-    // received pieces: [0, m) recovery (only [0, R) exist), [m, m+K) originals
-    typename TL::Reg v;
-#pragma unroll
-    for (int r = 0; r < TL::NR; ++r) {
-        const unsigned p = TL::piece(0, r, w);
-        const uint8_t* src = a.zeros;
-        uint64_t qq = 0;
-        if (!erased8(a, p)) {
-            if (p < a.R) { src = a.rec.ptr(p); qq = ql; }
-            else if (p >= a.m && p < a.m + a.K) { src = a.orig.ptr(p - a.m); qq = ql; }
-        }
-        load_units<F, C>(v[r], src, qq);
-    }
-    sk_stage.store(sk_tabs);
-    log_stage.store(ltab);
-    if (threadIdx.x == 0) {
-        reinterpret_cast<uint4*>(ltab.base)[256] = make_uint4(0, 0, 0, 0);
-        ltab.base[4 * 257 + 256] = 0;
-    }
-    if (w == 0) El8::compute(a, walsh, lane, el);
-    __syncthreads();
-    // absent pieces are zero: scaling them by anything keeps them zero
-#pragma unroll
-    for (int r = 0; r < TL::NR; ++r) {
-        F::mul(v[r], v[r], ltab.at(int(el[TL::piece(0, r, w)])));
-    }
-    win.stage(nullptr, -1);
-    TL::ifft(v, w, lane, lds, ps, win);
-    TL::derivative_inplace(v, w, lane, lds);
-    TL::fft(v, w, lane, lds, ps, win);
-    TL::pin(v);
-    if (!live) return;
-#pragma unroll
-    for (int r = 0; r < TL::NR; ++r) {
-        const unsigned p = TL::piece(0, r, w);
-        if (p >= a.m && p < a.m + a.K && erased8(a, p)) {  // LeopardFF8.cpp:1913-1915
-            uint32_t y[C];
-            F::mul(y, v[r], ltab.at(int(F::kModulus - el[p])));
-            store_units<F, C>(a.out.ptr(p - a.m), q0, y);
-        }
-        __builtin_amdgcn_sched_barrier(0);  // no hoisting of later pieces' addresses
-    }
-}
-
 // pass 1: scale-on-load + IFFT over the low bits -> a_out[g]
 template <class F>
 __global__ void __launch_bounds__(64 << wave_bits(kLoBits), 4) k_dec_lo(DecArgs a) {
@@ -414,7 +283,7 @@ __global__ void __launch_bounds__(64 << wave_bits(kLoBits), 4) k_dec_lo(DecArgs 
         __builtin_amdgcn_sched_barrier(0);
     }
     win.stage(a.sktab, -1);
-    TL::ifft(v, w, lane, lds, ps, win);
+    TL::ifft(v, w, lane, lds, ps, win, Pyr16Live{a.present_pyr});
     if (!live) return;
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) store_units<F, C>(a.a_out.ptr(ps.global(TL::piece(TL::kLast, r, w))), q0, v[r]);
@@ -438,14 +307,14 @@ __global__ void __launch_bounds__(64 << wave_bits(T), 4) k_dec_hi(DecArgs a) {
         load_or_zero<F>(v[r], a.a_in, tp < a.nlo, ps.global(tp), a.zeros, ql);
     }
     win.stage(a.sktab, -1);
-    TL::ifft(v, w, lane, lds, ps, win);
+    TL::ifft(v, w, lane, lds, ps, win, Pyr16Live{a.present_pyr});
     TL::copy(d, v);
     TL::derivative_add(d, v, w, lane, lds);
-    TL::fft(d, w, lane, lds, ps, win);
+    TL::fft(d, w, lane, lds, ps, win, Pyr16Live{a.needed_pyr});
     if (live)
 #pragma unroll
         for (int r = 0; r < TL::NR; ++r) store_units<F, C>(a.a_out.ptr(ps.global(TL::piece(0, r, w))), q0, d[r]);
-    TL::fft(v, w, lane, lds, ps, win);
+    TL::fft(v, w, lane, lds, ps, win, Pyr16Live{a.needed_pyr});
     if (live)
 #pragma unroll
         for (int r = 0; r < TL::NR; ++r) store_units<F, C>(a.b_out.ptr(ps.global(TL::piece(0, r, w))), q0, v[r]);
@@ -478,7 +347,7 @@ __global__ void __launch_bounds__(64 << wave_bits(kLoBits), 4) k_dec_fin(DecArgs
     }
     win.stage(a.sktab, -1);
     TL::derivative_add(z, v, w, lane, lds);
-    TL::fft(z, w, lane, lds, ps, win);
+    TL::fft(z, w, lane, lds, ps, win, Pyr16Live{a.needed_pyr});
     if (!live) return;
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) {
@@ -583,13 +452,6 @@ struct EncFusedFn {
     }
 };
 template <class F, int T>
-struct DecFused8Fn {
-    static hipError_t run(const DecArgs& a, hipStream_t s) {
-        return launch(&k_dec_fused8<T>, dim3(tiles_for(a.nunits)), 64u << wave_bits(T),
-                      full_tile_lds<FF8, T>() + LdsTab8<257>::kDwords + 256, s, &a);
-    }
-};
-template <class F, int T>
 struct EncHiFn {
     static hipError_t run(const EncArgs& a, hipStream_t s) {
         return launch(&k_enc_hi<F, T>, dim3(tiles_for(a.nunits), 1u << kLoBits), 64u << wave_bits(T),
@@ -615,9 +477,8 @@ hipError_t dispatch_T(unsigned T, const A& a, hipStream_t s) {
 
 }  // namespace
 
-hipError_t launch_encode_fused(int ff16, unsigned T, const EncArgs& a, hipStream_t s) {
-    if (ff16) return dispatch_T<EncFusedFn, FF16, 1, 8>(T, a, s);
-    return dispatch_T<EncFusedFn, FF8, 1, 7>(T, a, s);
+hipError_t launch_encode_fused16(unsigned T, const EncArgs& a, hipStream_t s) {
+    return dispatch_T<EncFusedFn, FF16, 1, 8>(T, a, s);
 }
 hipError_t launch_encode_lo(const EncArgs& a, hipStream_t s) {
     const unsigned m = 1u << a.Tm;
@@ -631,9 +492,6 @@ hipError_t launch_encode_fin(const EncArgs& a, hipStream_t s) {
     const unsigned tiles = (a.R + (1u << kLoBits) - 1) >> kLoBits;
     return launch(&k_enc_fin<FF16>, dim3(tiles_for(a.nunits), tiles), 64u << wave_bits(kLoBits),
                   full_tile_lds<FF16, kLoBits>(), s, &a);
-}
-hipError_t launch_decode_fused8(unsigned T, const DecArgs& a, hipStream_t s) {
-    return dispatch_T<DecFused8Fn, FF8, 1, 8>(T, a, s);
 }
 hipError_t launch_decode_lo(const DecArgs& a, hipStream_t s) {
     return launch(&k_dec_lo<FF16>, dim3(tiles_for(a.nunits), a.nlo), 64u << wave_bits(kLoBits),

@@ -12,7 +12,7 @@ import leopard_amd as leo  # noqa: E402
 from bench import hash_fill_cuda  # noqa: E402
 
 
-def run(k, r, b, sets=16, n=100):
+def run(k, r, b, sets=16, n=100, warm=int(os.environ.get('KB_WARM', '300'))):
     VP = ctypes.c_void_p
     lib = leo.lib
     ewc, dwc = leo.leo_encode_work_count(k, r), leo.leo_decode_work_count(k, r)
@@ -35,7 +35,7 @@ def run(k, r, b, sets=16, n=100):
     st = torch.cuda.current_stream()
 
     def t(fn):
-        for j in range(10):
+        for j in range(warm):
             fn(j % sets)
         a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(st)

@@ -8,11 +8,16 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/leopard.h"
@@ -108,9 +113,37 @@ struct Workspace {
     size_t hsize = 0;
     hipEvent_t stage_done = nullptr;
     bool stage_pending = false;
+    // Host-memory pipeline ring: two slots of `slot_bytes` in pinned host memory
+    // and in device memory, one stream and two events per slot.
+    uint8_t* ring_host = nullptr;
+    uint8_t* ring_dev = nullptr;
+    size_t slot_bytes = 0;
+    hipStream_t pipe_stream[2] = {nullptr, nullptr};
+    hipEvent_t in_done[2] = {nullptr, nullptr};
+    hipEvent_t out_done[2] = {nullptr, nullptr};
 
     ~Workspace() {
         // Process teardown: the runtime may already be gone; leak rather than crash.
+    }
+    LeopardResult reserve_ring(size_t bytes_per_slot) {
+        for (int s = 0; s < 2; ++s) {
+            if (!pipe_stream[s]) HIP_OK(hipStreamCreateWithFlags(&pipe_stream[s], hipStreamNonBlocking), "stream");
+            if (!in_done[s]) HIP_OK(hipEventCreateWithFlags(&in_done[s], hipEventDisableTiming), "event");
+            if (!out_done[s]) HIP_OK(hipEventCreateWithFlags(&out_done[s], hipEventDisableTiming), "event");
+        }
+        if (bytes_per_slot <= slot_bytes) return Leopard_Success;
+        if (ring_dev) {
+            HIP_OK(hipDeviceSynchronize(), "sync before ring growth");
+            HIP_OK(hipFree(ring_dev), "free ring");
+            HIP_OK(hipHostFree(ring_host), "free pinned ring");
+            ring_dev = ring_host = nullptr;
+            slot_bytes = 0;
+        }
+        const size_t want = (bytes_per_slot + 4095) / 4096 * 4096;
+        HIP_OK(hipMalloc(reinterpret_cast<void**>(&ring_dev), 2 * want), "allocate device ring");
+        HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&ring_host), 2 * want, hipHostMallocDefault), "pinned ring");
+        slot_bytes = want;
+        return Leopard_Success;
     }
     LeopardResult reserve_device(size_t bytes) {
         if (bytes <= dsize) return Leopard_Success;
@@ -530,23 +563,151 @@ LeopardResult decode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
     return Leopard_Success;
 }
 
-// ----------------------------------------------------- host-memory staging --
+// ---------------------------------------------------- host-memory pipeline --
 
-// Host buffers: stage through device memory (reference contract: caller-owned
-// host pieces in, results in host memory on return).
-struct HostStage {
-    uint8_t* dev = nullptr;
-    size_t size = 0;
-    ~HostStage() {
-        if (dev) (void)hipFree(dev);
+// Host (pageable) pieces are the reference's contract: caller-owned buffers in,
+// results in host memory on return.  The columns are cut into slices that flow
+// through a two-slot ring: host threads gather one slice of every input piece
+// into pinned memory, one H2D copy, the kernels, one D2H copy, host threads
+// scatter the outputs.  Slot j & 1 has its own stream, so the gather of slice
+// j, the copies and kernels of slice j - 1 and the scatter of slice j - 1 overlap.
+
+// Fixed pool of host copy threads (LEO_AMD_HOST_THREADS, default min(8, cores)).
+class CpuPool {
+public:
+    static CpuPool& get() {
+        static CpuPool* pool = new CpuPool();  // never destroyed: detached workers outlive static teardown
+        return *pool;
     }
+    // fn(i) for every i in [0, count), on the workers and the calling thread.
+    void run(unsigned count, const std::function<void(unsigned)>& fn) {
+        if (workers_ == 0 || count <= 1) {
+            for (unsigned i = 0; i < count; ++i) fn(i);
+            return;
+        }
+        std::lock_guard<std::mutex> call(call_mu_);
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            fn_ = &fn;
+            count_ = count;
+            next_.store(0);
+            busy_ = workers_;
+            ++gen_;
+        }
+        cv_.notify_all();
+        drain();
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [&] { return busy_ == 0; });
+        fn_ = nullptr;
+    }
+
+private:
+    CpuPool() {
+        unsigned n = std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
+        if (const char* e = std::getenv("LEO_AMD_HOST_THREADS")) n = unsigned(std::max(1, std::atoi(e)));
+        workers_ = n - 1;
+        for (unsigned i = 0; i < workers_; ++i) std::thread([this] { loop(); }).detach();
+    }
+    void drain() {
+        for (unsigned i = next_.fetch_add(1); i < count_; i = next_.fetch_add(1)) (*fn_)(i);
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return gen_ != seen; });
+                seen = gen_;
+            }
+            drain();
+            std::lock_guard<std::mutex> lk(mu_);
+            if (--busy_ == 0) done_.notify_one();
+        }
+    }
+    std::mutex call_mu_, mu_;
+    std::condition_variable cv_, done_;
+    const std::function<void(unsigned)>* fn_ = nullptr;
+    unsigned count_ = 0, workers_ = 0, busy_ = 0;
+    std::atomic<unsigned> next_{0};
+    uint64_t gen_ = 0;
 };
 
-LeopardResult copy_pieces(hipStream_t s, void* const* dst, const void* const* src, unsigned count, uint64_t bytes,
-                          hipMemcpyKind kind) {
-    for (unsigned i = 0; i < count; ++i)
-        if (src[i] && dst[i]) HIP_OK(hipMemcpyAsync(dst[i], src[i], bytes, kind, s), "piece copy");
-    return Leopard_Success;
+struct CopyJob {
+    uint8_t* dst;
+    const uint8_t* src;
+    uint64_t len;
+};
+
+// memcpy of every job, split into <= 1 MiB parts spread over the pool.
+void parallel_copy(const std::vector<CopyJob>& jobs) {
+    constexpr uint64_t kPart = 1 << 20;
+    std::vector<CopyJob> parts;
+    for (const CopyJob& j : jobs)
+        for (uint64_t o = 0; o < j.len; o += kPart) parts.push_back({j.dst + o, j.src + o, std::min(kPart, j.len - o)});
+    CpuPool::get().run(unsigned(parts.size()), [&](unsigned i) { std::memcpy(parts[i].dst, parts[i].src, parts[i].len); });
+}
+
+// Device work for one slice: inputs are rows [0, nin) of `din`, outputs rows
+// [0, nout) of `dout`, row stride `stride`, `len` bytes per row.
+using SliceFn = std::function<LeopardResult(Call&, uint64_t len, uint8_t* din, uint8_t* dout, uint64_t stride)>;
+
+// Bytes per ring slot (inputs + outputs of one slice); LEO_AMD_SLOT_MB overrides.
+uint64_t pipe_slot_budget() {
+    static const uint64_t v = [] {
+        const char* e = std::getenv("LEO_AMD_SLOT_MB");
+        const long mb = e ? std::atol(e) : 32;
+        return uint64_t(std::max(1L, mb)) << 20;
+    }();
+    return v;
+}
+
+// hin: host input pieces (call offset applied); hout: host output pieces.
+// two_streams: the slice work uses no shared scratch, so slots may overlap.
+LeopardResult run_host_pipeline(Call& c, uint64_t bytes, const std::vector<const uint8_t*>& hin,
+                                const std::vector<uint8_t*>& hout, bool two_streams, const SliceFn& fn) {
+    const uint64_t nin = hin.size(), nout = hout.size(), rows = nin + nout;
+    uint64_t slice = bytes;
+    if (rows * bytes > pipe_slot_budget())  // >= 4 KiB slices even when that outgrows the budget
+        slice = std::max<uint64_t>(pipe_slot_budget() / rows / 64 * 64, std::min<uint64_t>(bytes, 4096));
+    if (rows * bytes > (4ull << 20)) slice = std::min<uint64_t>(slice, (bytes / 4 + 63) / 64 * 64);  // >= 4 slices
+    const uint64_t in_bytes = nin * slice, slot = rows * slice;
+    LeopardResult r = c.ws->reserve_ring(slot);
+    if (r != Leopard_Success) return r;
+    Workspace& ws = *c.ws;
+    const unsigned nslices = unsigned((bytes + slice - 1) / slice);
+    auto len_of = [&](unsigned j) { return std::min(slice, bytes - uint64_t(j) * slice); };
+    auto stream_of = [&](unsigned s) { return two_streams ? ws.pipe_stream[s] : ws.pipe_stream[0]; };
+    auto scatter = [&](unsigned j) -> LeopardResult {
+        const unsigned s = j & 1;
+        HIP_OK(hipEventSynchronize(ws.out_done[s]), "wait slice output");
+        const uint8_t* pin = ws.ring_host + s * ws.slot_bytes + in_bytes;
+        std::vector<CopyJob> jobs;
+        for (uint64_t i = 0; i < nout; ++i) jobs.push_back({hout[i] + uint64_t(j) * slice, pin + i * slice, len_of(j)});
+        parallel_copy(jobs);
+        return Leopard_Success;
+    };
+    for (unsigned j = 0; j < nslices; ++j) {
+        const unsigned s = j & 1;
+        uint8_t* pin = ws.ring_host + s * ws.slot_bytes;
+        uint8_t* dev = ws.ring_dev + s * ws.slot_bytes;
+        const uint64_t pos = uint64_t(j) * slice, len = len_of(j);
+        if (j >= 2) HIP_OK(hipEventSynchronize(ws.in_done[s]), "wait slot input");
+        std::vector<CopyJob> jobs;
+        for (uint64_t i = 0; i < nin; ++i) jobs.push_back({pin + i * slice, hin[i] + pos, len});
+        parallel_copy(jobs);
+        Call cs = c;
+        cs.s = stream_of(s);
+        HIP_OK(hipMemcpyAsync(dev, pin, in_bytes, hipMemcpyHostToDevice, cs.s), "slice upload");
+        HIP_OK(hipEventRecord(ws.in_done[s], cs.s), "record upload");
+        r = fn(cs, len, dev, dev + in_bytes, slice);
+        if (r != Leopard_Success) return r;
+        HIP_OK(hipGetLastError(), "kernel launch");
+        HIP_OK(hipMemcpyAsync(pin + in_bytes, dev + in_bytes, nout * slice, hipMemcpyDeviceToHost, cs.s),
+               "slice download");
+        HIP_OK(hipEventRecord(ws.out_done[s], cs.s), "record download");
+        if (j >= 1 && (r = scatter(j - 1)) != Leopard_Success) return r;
+    }
+    return scatter(nslices - 1);
 }
 
 LeopardResult encode_any(uint64_t bytes, uint64_t off, unsigned K, unsigned R, const void* const* orig, void** work);
@@ -599,31 +760,28 @@ LeopardResult encode_any(uint64_t bytes, uint64_t off, unsigned K, unsigned R, c
         return finish(c, false);
     }
 
-    // host memory: stage K inputs + R outputs in a device slab
-    HostStage st;
-    HIP_OK(hipMalloc(reinterpret_cast<void**>(&st.dev), uint64_t(K + R) * bytes), "host staging");
-    std::vector<const void*> din(K), hsrc(K);
-    std::vector<void*> dout(R), hdst(R), ddst(K);
-    for (unsigned i = 0; i < K; ++i) {
-        din[i] = st.dev + uint64_t(i) * bytes;
-        ddst[i] = const_cast<void*>(din[i]);
-        hsrc[i] = static_cast<const uint8_t*>(orig[i]) + off;
-    }
-    for (unsigned i = 0; i < R; ++i) {
-        dout[i] = st.dev + uint64_t(K + i) * bytes;
-        hdst[i] = static_cast<uint8_t*>(work[i]) + off;
-    }
-    r = copy_pieces(c.s, ddst.data(), hsrc.data(), K, bytes, hipMemcpyHostToDevice);
-    if (r != Leopard_Success) return r;
+    // host memory (leopard.cpp:143-149: K == 1 is a copy)
     if (K == 1) {
-        for (unsigned i = 0; i < R; ++i) dout[i] = const_cast<void*>(din[i]);
-    } else if (R == 1) {
-        r = xor_device(c, bytes, 0, din.data(), K, dout[0]);
-    } else {
-        r = encode_device(c, bytes, 0, K, R, din.data(), dout.data());
+        std::vector<CopyJob> jobs;
+        for (unsigned i = 0; i < R; ++i)
+            jobs.push_back({static_cast<uint8_t*>(work[i]) + off, static_cast<const uint8_t*>(orig[i]) + off, bytes});
+        parallel_copy(jobs);
+        return Leopard_Success;
     }
-    if (r != Leopard_Success) return r;
-    r = copy_pieces(c.s, hdst.data(), const_cast<const void* const*>(dout.data()), R, bytes, hipMemcpyDeviceToHost);
+    std::vector<const uint8_t*> hin(K);
+    std::vector<uint8_t*> hout(R);
+    for (unsigned i = 0; i < K; ++i) hin[i] = static_cast<const uint8_t*>(orig[i]) + off;
+    for (unsigned i = 0; i < R; ++i) hout[i] = static_cast<uint8_t*>(work[i]) + off;
+    const bool ff16 = next_pow2(next_pow2(R) + K) > 256;
+    r = run_host_pipeline(c, bytes, hin, hout, R == 1 || !ff16,
+                          [&](Call& cs, uint64_t len, uint8_t* din, uint8_t* dout, uint64_t stride) {
+                              std::vector<const void*> di(K);
+                              std::vector<void*> dw(R);
+                              for (unsigned i = 0; i < K; ++i) di[i] = din + i * stride;
+                              for (unsigned i = 0; i < R; ++i) dw[i] = dout + i * stride;
+                              if (R == 1) return xor_device(cs, len, 0, di.data(), K, dw[0]);
+                              return encode_device(cs, len, 0, K, R, di.data(), dw.data());
+                          });
     if (r != Leopard_Success) return r;
     return finish(c, true);
 }
@@ -675,57 +833,53 @@ LeopardResult decode_any(uint64_t bytes, uint64_t off, unsigned K, unsigned R, c
         return finish(c, false);
     }
 
-    // host memory: present originals, present recoveries and the lost outputs
-    HostStage st;
-    HIP_OK(hipMalloc(reinterpret_cast<void**>(&st.dev), uint64_t(K + R) * bytes), "host staging");
-    std::vector<const void*> dorig(K, nullptr), drec(R, nullptr), hsrc;
-    std::vector<void*> dwork(K, nullptr), ddst, hdst;
-    for (unsigned i = 0; i < K; ++i) {
-        uint8_t* slot = st.dev + uint64_t(i) * bytes;
-        dwork[i] = slot;  // lost i is rebuilt in place of its original
-        if (orig[i]) {
-            dorig[i] = slot;
-            ddst.push_back(slot);
-            hsrc.push_back(static_cast<const uint8_t*>(orig[i]) + off);
+    // host memory: K == 1 and zero loss are copies (leopard.cpp:279-291)
+    if (K == 1 || lost == 0) {
+        std::vector<CopyJob> jobs;
+        if (K == 1) jobs.push_back({static_cast<uint8_t*>(work[0]) + off, static_cast<const uint8_t*>(k1_src) + off, bytes});
+        else
+            for (unsigned i = 0; i < K; ++i)
+                jobs.push_back({static_cast<uint8_t*>(work[i]) + off, static_cast<const uint8_t*>(orig[i]) + off, bytes});
+        parallel_copy(jobs);
+        return Leopard_Success;
+    }
+    // Slice rows: received recoveries first, then received originals (so the
+    // R == 1 XOR sources form one slab), outputs = lost originals in order.
+    std::vector<const uint8_t*> hin;
+    std::vector<uint8_t*> hout;
+    std::vector<int> in_row_rec(R, -1), in_row_orig(K, -1), out_row(K, -1);
+    for (unsigned i = 0; i < R; ++i)
+        if (rec[i]) {
+            in_row_rec[i] = int(hin.size());
+            hin.push_back(static_cast<const uint8_t*>(rec[i]) + off);
         }
-    }
-    for (unsigned i = 0; i < R; ++i) {
-        if (!rec[i]) continue;
-        uint8_t* slot = st.dev + uint64_t(K + i) * bytes;
-        drec[i] = slot;
-        ddst.push_back(slot);
-        hsrc.push_back(static_cast<const uint8_t*>(rec[i]) + off);
-    }
-    r = copy_pieces(c.s, ddst.data(), hsrc.data(), unsigned(ddst.size()), bytes, hipMemcpyHostToDevice);
-    if (r != Leopard_Success) return r;
-    std::vector<const void*> dres;
-    std::vector<void*> hout;
-    if (K == 1) {
-        dres.push_back(rec[got_i] ? drec[got_i] : dorig[0]);
-        hout.push_back(static_cast<uint8_t*>(work[0]) + off);
-    } else if (lost == 0) {
-        for (unsigned i = 0; i < K; ++i) {
-            dres.push_back(dorig[i]);
+    for (unsigned i = 0; i < K; ++i) {
+        if (orig[i]) {
+            in_row_orig[i] = int(hin.size());
+            hin.push_back(static_cast<const uint8_t*>(orig[i]) + off);
+        } else {
+            out_row[i] = int(hout.size());
             hout.push_back(static_cast<uint8_t*>(work[i]) + off);
         }
-    } else if (R == 1) {
-        std::vector<const void*> src;
-        src.push_back(drec[0]);
-        for (unsigned i = 0; i < K; ++i)
-            if (dorig[i]) src.push_back(dorig[i]);
-        r = xor_device(c, bytes, 0, src.data(), unsigned(src.size()), dwork[lost_i]);
-        dres.push_back(dwork[lost_i]);
-        hout.push_back(static_cast<uint8_t*>(work[lost_i]) + off);
-    } else {
-        r = decode_device(c, bytes, 0, K, R, dorig.data(), drec.data(), dwork.data());
-        for (unsigned i = 0; i < K; ++i)
-            if (!orig[i]) {
-                dres.push_back(dwork[i]);
-                hout.push_back(static_cast<uint8_t*>(work[i]) + off);
-            }
     }
-    if (r != Leopard_Success) return r;
-    r = copy_pieces(c.s, hout.data(), dres.data(), unsigned(dres.size()), bytes, hipMemcpyDeviceToHost);
+    const bool ff16 = next_pow2(next_pow2(R) + K) > 256;
+    r = run_host_pipeline(c, bytes, hin, hout, R == 1 || !ff16,
+                          [&](Call& cs, uint64_t len, uint8_t* din, uint8_t* dout, uint64_t stride) {
+                              if (R == 1) {  // leopard.cpp:294-303
+                                  std::vector<const void*> src;
+                                  for (size_t j = 0; j < hin.size(); ++j) src.push_back(din + j * stride);
+                                  return xor_device(cs, len, 0, src.data(), unsigned(src.size()), dout);
+                              }
+                              std::vector<const void*> dorig(K, nullptr), drec(R, nullptr);
+                              std::vector<void*> dwork(K, nullptr);
+                              for (unsigned i = 0; i < R; ++i)
+                                  if (in_row_rec[i] >= 0) drec[i] = din + in_row_rec[i] * stride;
+                              for (unsigned i = 0; i < K; ++i) {
+                                  if (in_row_orig[i] >= 0) dorig[i] = din + in_row_orig[i] * stride;
+                                  else dwork[i] = dout + out_row[i] * stride;
+                              }
+                              return decode_device(cs, len, 0, K, R, dorig.data(), drec.data(), dwork.data());
+                          });
     if (r != Leopard_Success) return r;
     return finish(c, true);
 }

@@ -326,6 +326,25 @@ struct TabStage8 {
     }
 };
 
+// LDS areas used in turn by consecutive tile exchanges (Tile::exchange,
+// Tile::derivative_ring).  With two areas an area is rewritten only after the
+// barrier of the exchange in between, so an exchange needs one barrier (writes
+// -> reads); with one area it also needs one ahead of its writes, but takes
+// half the LDS (more workgroups per CU).  The counter is a compile-time
+// constant once the transforms are unrolled.
+template <size_t kArea, int kAreas>
+struct LdsRing {
+    static_assert(kAreas == 1 || kAreas == 2, "one or two areas");
+    static constexpr bool kPreBarrier = kAreas == 1;
+    uint32_t* base;
+    unsigned n = 0;
+    LDEV uint32_t* next() {
+        uint32_t* p = base + (kAreas == 2 ? (n & 1u) * kArea : 0);
+        ++n;
+        return p;
+    }
+};
+
 // Global piece index of tile piece tp:  lo_fixed | tp << l0 | hi_fixed.
 struct PieceSpace {
     unsigned lo_fixed, l0, hi_fixed;
@@ -338,15 +357,21 @@ struct PieceSpace {
 // stays all-zero, so its butterflies are skipped; FFT: a block holding no
 // needed output feeds no needed output, so its butterflies are skipped (the
 // reference's FFT_DIT_ErrorBits, LeopardFF8.cpp:1681-1801, generalised to both
-// transforms).  Every predicate is wave-uniform (scalar).
+// transforms).  Every predicate is wave-uniform (scalar).  The pipelined
+// transforms fetch a predicate's raw word with the lookahead of its layer
+// (word) and test it when the layer runs (bit).
 struct AllLive {
     LDEV constexpr bool operator()(unsigned, unsigned) const { return true; }
+    LDEV constexpr uint32_t word(unsigned, unsigned) const { return 1u; }
+    LDEV constexpr bool bit(uint32_t, unsigned, unsigned) const { return true; }
 };
 // Live iff the block starts below `limit` (encoder: inputs [0, K - base),
 // outputs [0, R)).
 struct BelowLive {
     unsigned limit;
     LDEV bool operator()(unsigned pos, unsigned level) const { return ((pos >> level) << level) < limit; }
+    LDEV uint32_t word(unsigned pos, unsigned level) const { return (*this)(pos, level) ? 1u : 0u; }
+    LDEV bool bit(uint32_t wd, unsigned, unsigned) const { return wd != 0; }
 };
 // Occupancy pyramid: level L holds one bit per aligned block of 2^L positions,
 // starting at word off(L).  FF8: 256 positions, 20 words, passed by value in
@@ -355,10 +380,9 @@ constexpr unsigned pyr8_offset(unsigned L) { return L <= 3 ? 16u - (16u >> L) : 
 constexpr unsigned kPyr8Words = 20;
 struct Pyr8Live {
     const uint32_t* w;  // kernel-argument words
-    LDEV bool operator()(unsigned pos, unsigned level) const {
-        const unsigned j = pos >> level;
-        return (w[pyr8_offset(level) + (j >> 5)] >> (j & 31)) & 1u;
-    }
+    LDEV uint32_t word(unsigned pos, unsigned level) const { return w[pyr8_offset(level) + ((pos >> level) >> 5)]; }
+    LDEV bool bit(uint32_t wd, unsigned pos, unsigned level) const { return (wd >> ((pos >> level) & 31)) & 1u; }
+    LDEV bool operator()(unsigned pos, unsigned level) const { return bit(word(pos, level), pos, level); }
 };
 
 // Skew index of the butterfly on pair (i, i + 2^l), bit l of i clear: the
@@ -542,6 +566,195 @@ struct Tile {
             const uint32_t* p = lds + (size_t(piece(TO, r, w)) * 64 + lane) * U;
 #pragma unroll
             for (int k = 0; k < U; ++k) x[r][k] = p[k];
+        }
+    }
+
+    // ------------------------------------------------------------------
+    // Pipelined transforms (GF(2^8) kernels: butterfly tables in LDS).
+    //  * The tables and predicate words of layer l+1 are read before the
+    //    butterflies of layer l, so the LDS / scalar reads overlap butterflies.
+    //    After a barrier all waves run in lockstep; reading a layer's tables at
+    //    its start stalled every wave on the LDS at once (measured: LDS and
+    //    VALU time added up).
+    //  * A layer's live-group mask is formed before the next lookahead is
+    //    issued: scalar loads return out of order, so a wait on one is a wait on
+    //    every outstanding LDS and scalar read (lgkmcnt(0)).
+    //  * Exchanges go through an LdsRing (one or two areas).
+    static constexpr size_t kAreaDwords = (size_t(1) << T) * 64 * U;
+    static constexpr int kMaxGroups = NR / 2 > 0 ? NR / 2 : 1;
+    struct Look {
+        typename F::Tab t[kMaxGroups];
+        uint32_t pw[kMaxGroups];
+    };
+
+    static constexpr int ifft_layout(int L) {
+        int k = 0;
+        while (!(L >= ifft_begin(k) && L < lo(k) + R)) ++k;
+        return k;
+    }
+    static constexpr int fft_layout(int L) {
+        int k = NL - 1;
+        while (!(L >= lo(k) && L < fft_end(k))) --k;
+        return k;
+    }
+    static constexpr int groups(int LAY, int L) { return NR / (2 << (L - lo(LAY))); }
+
+    template <int LAY, int L, class Win, class Pred>
+    LDEV static void read_look(Look& lk, unsigned w, const PieceSpace& ps, const Win& win, const Pred& pred) {
+        constexpr int half = 1 << (L - lo(LAY));
+        asm volatile("" ::: "memory");  // keep the reads here (issue point of the lookahead)
+        static_for<0, groups(LAY, L)>([&](auto G) {
+            constexpr int gi = decltype(G)::value;
+            const unsigned pos = ps.global(piece(LAY, gi * 2 * half, w));
+            lk.t[gi] = win.table(skew_index(pos, ps.l0 + L));
+            lk.pw[gi] = pred.word(pos, ps.l0 + L + 1);
+        });
+    }
+    template <int LAY, int L>
+    LDEV static void take_look(Look& cur, const Look& nxt) {
+        static_for<0, groups(LAY, L)>([&](auto G) {
+            cur.t[decltype(G)::value] = nxt.t[decltype(G)::value];
+            cur.pw[decltype(G)::value] = nxt.pw[decltype(G)::value];
+        });
+    }
+    template <int LAY, int L, class Pred>
+    LDEV static uint32_t live_mask(const Look& lk, unsigned w, const PieceSpace& ps, const Pred& pred) {
+        constexpr int half = 1 << (L - lo(LAY));
+        uint32_t mask = 0;
+        static_for<0, groups(LAY, L)>([&](auto G) {
+            constexpr int gi = decltype(G)::value;
+            const unsigned pos = ps.global(piece(LAY, gi * 2 * half, w));
+            if (pred.bit(lk.pw[gi], pos, ps.l0 + L + 1)) mask |= 1u << gi;
+        });
+        asm volatile("" ::"s"(mask));  // formed here, ahead of the next lookahead
+        return mask;
+    }
+    template <bool kInverse, int LAY, int L>
+    LDEV static void apply(Reg& x, const Look& lk, uint32_t live) {
+        if constexpr ((LAMD_ABLATE & 1) != 0) return;
+        constexpr int half = 1 << (L - lo(LAY));
+        static_for<0, groups(LAY, L)>([&](auto G) {
+            constexpr int gi = decltype(G)::value, g = gi * 2 * half;
+            if ((live >> gi) & 1u) {
+#pragma unroll
+                for (int j = 0; j < half; ++j) {
+#pragma unroll
+                    for (int u = 0; u < C; ++u) {
+                        uint32_t* a = &x[g + j][u * F::kDw];
+                        uint32_t* b = &x[g + j + half][u * F::kDw];
+                        if constexpr (kInverse) {
+#pragma unroll
+                            for (int k = 0; k < F::kDw; ++k) {
+                                b[k] ^= a[k];
+                                if constexpr (F::kDw == 1) asm volatile("" : "+v"(b[k]));
+                            }
+                            F::muladd(a, b, lk.t[gi]);
+                        } else {
+                            F::muladd(a, b, lk.t[gi]);
+#pragma unroll
+                            for (int k = 0; k < F::kDw; ++k) b[k] ^= a[k];
+                        }
+                    }
+                }
+            }
+        });
+    }
+
+    // Transpose from layout FROM to layout TO through the ring's next area.
+    template <int FROM, int TO, class Ring>
+    LDEV static void exchange(Reg& x, unsigned w, unsigned lane, Ring& ring) {
+        uint32_t* area = ring.next();
+        if constexpr ((LAMD_ABLATE & 2) != 0) return;
+        if constexpr (Ring::kPreBarrier) __syncthreads();
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            uint32_t* p = area + (size_t(piece(FROM, r, w)) * 64 + lane) * U;
+#pragma unroll
+            for (int k = 0; k < U; ++k) p[k] = x[r][k];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            const uint32_t* p = area + (size_t(piece(TO, r, w)) * 64 + lane) * U;
+#pragma unroll
+            for (int k = 0; k < U; ++k) x[r][k] = p[k];
+        }
+    }
+
+    template <bool kSkipTop = false, class Ring, class Win, class Pred = AllLive>
+    LDEV static void ifft_pl(Reg& x, unsigned w, unsigned lane, Ring& ring, const PieceSpace& ps, const Win& win,
+                             const Pred& pred = Pred{}) {
+        constexpr int NS = kSkipTop ? T - 1 : T;  // layers computed here
+        Look cur, nxt;
+        if constexpr (NS > 0) read_look<ifft_layout(0), 0>(cur, w, ps, win, pred);
+        static_for<0, (NS > 0 ? NS : 0)>([&](auto S) {
+            constexpr int L = decltype(S)::value, k = ifft_layout(L);
+            const uint32_t live = live_mask<k, L>(cur, w, ps, pred);
+            if constexpr (L + 1 < NS) read_look<ifft_layout(L + 1), L + 1>(nxt, w, ps, win, pred);
+            apply<true, k, L>(x, cur, live);
+            if constexpr (L + 1 < T && ifft_layout(L + 1) != k) exchange<k, ifft_layout(L + 1)>(x, w, lane, ring);
+            if constexpr (L + 1 < NS) take_look<ifft_layout(L + 1), L + 1>(cur, nxt);
+        });
+        if constexpr (NS == 0 && NL > 1) exchange<0, kLast>(x, w, lane, ring);
+    }
+
+    template <bool kSkipTop = false, class Ring, class Win, class Pred = AllLive>
+    LDEV static void fft_pl(Reg& x, unsigned w, unsigned lane, Ring& ring, const PieceSpace& ps, const Win& win,
+                            const Pred& pred = Pred{}) {
+        constexpr int top = kSkipTop ? T - 2 : T - 1;  // first layer computed here
+        if constexpr (top >= 0) {
+            if constexpr (fft_layout(top) != kLast) exchange<kLast, fft_layout(top)>(x, w, lane, ring);
+            Look cur, nxt;
+            read_look<fft_layout(top), top>(cur, w, ps, win, pred);
+            static_for<0, top + 1>([&](auto S) {
+                constexpr int L = top - decltype(S)::value, k = fft_layout(L);
+                const uint32_t live = live_mask<k, L>(cur, w, ps, pred);
+                if constexpr (L > 0) read_look<fft_layout(L - 1), L - 1>(nxt, w, ps, win, pred);
+                apply<false, k, L>(x, cur, live);
+                if constexpr (L > 0 && fft_layout(L - 1) != k) exchange<k, fft_layout(L - 1)>(x, w, lane, ring);
+                if constexpr (L > 0) take_look<fft_layout(L - 1), L - 1>(cur, nxt);
+            });
+            if constexpr (fft_layout(0) != 0) exchange<fft_layout(0), 0>(x, w, lane, ring);
+        } else if constexpr (NL > 1) {
+            exchange<kLast, 0>(x, w, lane, ring);
+        }
+    }
+
+    // v = (I + D) v in layout kLast through the ring's next area (one barrier
+    // with two areas).  Register bits: ascending r reads v[r | 2^b] before it
+    // is modified; wave bits: gathered from the LDS copy of the original v.
+    template <class Ring>
+    LDEV static void derivative_ring(Reg& v, unsigned w, unsigned lane, Ring& ring) {
+        uint32_t* area = ring.next();
+        if constexpr ((LAMD_ABLATE & 64) != 0) return;
+        if constexpr (T > R) {
+            if constexpr (Ring::kPreBarrier) __syncthreads();
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                uint32_t* p = area + (size_t(piece(kLast, r, w)) * 64 + lane) * U;
+#pragma unroll
+                for (int k = 0; k < U; ++k) p[k] = v[r][k];
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < NR; ++r)
+#pragma unroll
+            for (int b = 0; b < R; ++b)
+                if (!(r & (1 << b)))
+#pragma unroll
+                    for (int k = 0; k < U; ++k) v[r][k] ^= v[r | (1 << b)][k];
+        if constexpr (T > R) {
+            __syncthreads();
+            for (int b = 0; b < T - R; ++b) {
+                if (w & (1u << b)) continue;  // wave-uniform
+                const unsigned w2 = w | (1u << b);
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    const uint32_t* p = area + (size_t(piece(kLast, r, w2)) * 64 + lane) * U;
+#pragma unroll
+                    for (int k = 0; k < U; ++k) v[r][k] ^= p[k];
+                }
+            }
         }
     }
 

@@ -44,21 +44,47 @@ __device__ uint64_t* g_stamps;
 
 namespace {
 
-#ifndef LAMD_FF8_RB7  // experiment hook: register bits of the 7-bit tile
-#define LAMD_FF8_RB7 3
+// Register bits per lane of a T-bit tile (the remaining piece bits index the
+// wave): 8 pieces per lane up to 16 waves, 16 pieces for the 8-bit decoder
+// tile.  The encoder's 7-bit tile also has a 16-pieces-per-lane form (8 waves,
+// one LDS transpose per transform instead of two) that wins once every CU runs
+// several workgroups (large pieces); with one workgroup per CU the 16-wave form
+// hides more latency (measured: 64 KiB pieces 10.5 vs 11.1 us, 1 MiB 87 vs 79 us).
+// Tables through the scalar cache instead of LDS measured slower (decode +15%).
+constexpr int reg_bits8(int T) { return T <= 3 ? T : (T - 3 <= 4 ? 3 : T - 4); }
+constexpr int wide_bits8(int T) { return T == 7 ? 4 : reg_bits8(T); }
+constexpr unsigned threads_for(int T, int RB) { return 64u << (T - RB); }
+constexpr size_t tile_dwords_for(int T, int RB) { return T > RB ? (size_t(1) << T) * 64 : 0; }
+constexpr unsigned threads8(int T) { return threads_for(T, reg_bits8(T)); }
+constexpr size_t tile_dwords8(int T) { return tile_dwords_for(T, reg_bits8(T)); }
+
+// Pipelined transforms (Tile::ifft_pl / fft_pl: lookahead of tables and
+// predicate words, exchanges through an LdsRing of NA areas) or the plain ones
+// (Tile::ifft / fft, one area), for A/B builds.
+#ifndef LAMD_FF8_PIPE
+#define LAMD_FF8_PIPE 1
 #endif
-#ifndef LAMD_FF8_SGPR_TABS  // experiment hook: butterfly tables through the scalar cache
-#define LAMD_FF8_SGPR_TABS 0
-#endif
-#ifndef LAMD_FF8_RB8
-#define LAMD_FF8_RB8 4
-#endif
-constexpr int reg_bits8(int T) {
-    return T <= 3 ? T : T == 7 ? LAMD_FF8_RB7 : T == 8 ? LAMD_FF8_RB8 : (T - 3 <= 4 ? 3 : T - 4);
+constexpr bool kPipe8 = LAMD_FF8_PIPE != 0;
+constexpr bool pipe8(int NA) { return kPipe8 && NA == 2; }
+constexpr int areas8(int NA) { return pipe8(NA) ? 2 : 1; }
+
+// By grid size: while a launch has at most one workgroup per CU, the pipelined
+// transforms with two exchange areas (one barrier per exchange); for larger
+// launches the plain transforms with one area, whose smaller LDS and register
+// footprint fits more workgroups per CU (measured at 1 MiB pieces: encode 78
+// vs 87 us, decode 195 vs 226 us; at 64 KiB the pipelined encode is 3% faster).
+constexpr uint32_t kOneWgPerCuUnits = 256 * 64;  // 256 CUs x one 64-dword strip
+
+// Piece pointers of the NR pieces a lane holds, fetched as one batch of scalar
+// loads: otherwise the compiler sinks each load into the branch that uses it,
+// a chain of dependent scalar-load round trips before the piece loads issue.
+template <int NR, class Idx>
+LDEV void fetch_ptrs(uint64_t (&pp)[NR], const uint64_t* ptr, Idx idx) {
+#pragma unroll
+    for (int r = 0; r < NR; ++r) pp[r] = ptr[idx(r)];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) asm volatile("" : "+s"(pp[r]));
 }
-constexpr int wave_bits8(int T) { return T - reg_bits8(T); }
-constexpr unsigned threads8(int T) { return 64u << wave_bits8(T); }
-constexpr size_t tile_dwords8(int T) { return wave_bits8(T) > 0 ? (size_t(1) << T) * 64 : 0; }
 
 // This lane's column inside the workgroup's 64-dword strip.  Lanes past the
 // end of the pieces (last strip, B/4 not a multiple of 64) read the last valid
@@ -84,53 +110,60 @@ LDEV void gstore(uint64_t piece, const Cols& c, uint32_t v) {
 
 // --------------------------------------------------------------- encode -----
 
-template <int T, bool kMulti>
-__global__ void __launch_bounds__(threads8(T), 4) k_ff8_enc(Ff8EncArgs a) {
+template <int T, int RB, bool kMulti, int NA>
+__global__ void __launch_bounds__(threads_for(T, RB), 4) k_ff8_enc(Ff8EncArgs a) {
     if constexpr ((LAMD_ABLATE & 16) != 0) return;
-    using TL = Tile<FF8, T, reg_bits8(T), 1>;
+    using TL = Tile<FF8, T, RB, 1>;
     constexpr unsigned m = 1u << T;
+    constexpr size_t kTile = tile_dwords_for(T, RB);
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    const LdsTab8<256> tabs{lds + tile_dwords8(T)};
+    const LdsTab8<256> tabs{lds + areas8(NA) * kTile};
+    LdsRing<kTile, areas8(NA)> ring{lds};
     STAMP(0);
-    TabStage8<threads8(T), 256> stage;
-    if constexpr (!LAMD_FF8_SGPR_TABS) stage.load(a.sktab);  // issued ahead of the piece loads
+    TabStage8<threads_for(T, RB), 256> stage;
+    stage.load(a.sktab);  // issued ahead of the piece loads
     const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const Cols cl = strip_cols(a.nunits, lane);
     const PieceSpace ps{0, 0, 0};
     typename TL::Reg x;
     auto load_chunk = [&](unsigned c) {
-        const unsigned base = c * m;
+        const unsigned base = c * m;  // base + tp < nchunks * m <= K + m - 1 < 256
+        uint64_t pp[TL::NR];
+        fetch_ptrs(pp, a.ptr, [&](int r) { return base + TL::piece(0, r, w); });
 #pragma unroll
         for (int r = 0; r < TL::NR; ++r) {
             const unsigned i = base + TL::piece(0, r, w);
-            x[r][0] = i < a.K ? gload(a.ptr[i], cl) : 0u;  // past K: zero padding (LeopardFF8.cpp:1631-1634)
+            x[r][0] = i < a.K ? gload(pp[r], cl) : 0u;  // past K: zero padding (LeopardFF8.cpp:1631-1634)
         }
+    };
+    // IFFT / FFT of one stage: pipelined (lookahead tables, ring of two LDS areas) or plain
+    auto ifft = [&](const auto& win, const auto& pred) {
+        if constexpr (pipe8(NA)) TL::template ifft_pl<true>(x, w, lane, ring, ps, win, pred);
+        else TL::template ifft<true>(x, w, lane, lds, ps, win, pred);
+    };
+    auto fft = [&](const auto& win, const auto& pred) {
+        if constexpr (pipe8(NA)) TL::template fft_pl<true>(x, w, lane, ring, ps, win, pred);
+        else TL::template fft<true>(x, w, lane, lds, ps, win, pred);
     };
     load_chunk(0);
     STAMP(1);
-    if constexpr (!LAMD_FF8_SGPR_TABS) {
-        stage.store(tabs);
-        __syncthreads();
-    }
+    stage.store(tabs);
+    __syncthreads();
     STAMP(2);
-#if LAMD_FF8_SGPR_TABS
-    GlobalWindow<FF8> win;
-#else
     LdsSkew8 win{tabs};
-#endif
     if constexpr (!kMulti) {
-        win.stage(a.sktab, int(m - 1));
-        TL::template ifft<true>(x, w, lane, lds, ps, win, BelowLive{a.K});
+        win.stage(nullptr, int(m - 1));
+        ifft(win, BelowLive{a.K});
         STAMP(3);
         TL::fused_top(x, FF8::tab_at(a.fused));
-        win.stage(a.sktab, -1);
-        TL::template fft<true>(x, w, lane, lds, ps, win, BelowLive{a.R});
+        win.stage(nullptr, -1);
+        fft(win, BelowLive{a.R});
         STAMP(4);
     } else {
         typename TL::Reg acc;
         for (unsigned c = 0;;) {
-            win.stage(a.sktab, int(m - 1 + c * m));
-            TL::template ifft<true>(x, w, lane, lds, ps, win, BelowLive{a.K - c * m});
+            win.stage(nullptr, int(m - 1 + c * m));
+            ifft(win, BelowLive{a.K - c * m});
             TL::fused_top(x, FF8::tab_at(a.fused + c * FF8::kTabDw));
             if (c == 0) TL::copy(acc, x);
             else TL::xor_into(acc, x);
@@ -138,15 +171,17 @@ __global__ void __launch_bounds__(threads8(T), 4) k_ff8_enc(Ff8EncArgs a) {
             load_chunk(c);
         }
         TL::copy(x, acc);
-        win.stage(a.sktab, -1);
-        TL::template fft<true>(x, w, lane, lds, ps, win, BelowLive{a.R});
+        win.stage(nullptr, -1);
+        fft(win, BelowLive{a.R});
     }
     TL::pin(x);
+    uint64_t pp[TL::NR];
+    fetch_ptrs(pp, a.ptr, [&](int r) { return a.K + TL::piece(0, r, w); });  // K + tp < K + m <= 256
     if (!cl.live) return;
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) {
         const unsigned tp = TL::piece(0, r, w);
-        if (tp < a.R) gstore(a.ptr[a.K + tp], cl, x[r][0]);
+        if (tp < a.R) gstore(pp[r], cl, x[r][0]);
     }
     STAMP(5);
 }
@@ -155,14 +190,32 @@ __global__ void __launch_bounds__(threads8(T), 4) k_ff8_enc(Ff8EncArgs a) {
 
 LDEV unsigned el_at(const Ff8DecArgs& a, unsigned p) { return (a.el[p >> 2] >> ((p & 3) * 8)) & 0xFFu; }
 
-template <int T>
+// v[r] *= table(log_of(r)) for the pieces with pred(r): the tables of KB pieces
+// are read together, then their multiplies run (one LDS round trip per batch).
+template <class TL, class LogFn, class PredFn>
+LDEV void scale_batched(typename TL::Reg& v, const LdsTab8<256>& ltab, LogFn log_of, PredFn pred) {
+    constexpr int KB = TL::NR < 4 ? TL::NR : 4;
+    static_for<0, TL::NR / KB>([&](auto BI) {
+        constexpr int r0 = decltype(BI)::value * KB;
+        FF8::Tab t[KB];
+        asm volatile("" ::: "memory");
+        static_for<0, KB>([&](auto I) { t[decltype(I)::value] = ltab.at(int(log_of(r0 + decltype(I)::value))); });
+        static_for<0, KB>([&](auto I) {
+            constexpr int r = r0 + decltype(I)::value;
+            if ((LAMD_ABLATE & 128) == 0 && pred(r)) FF8::mul(v[r], v[r], t[decltype(I)::value]);
+        });
+    });
+}
+
+template <int T, int NA>
 __global__ void __launch_bounds__(threads8(T), 4) k_ff8_dec(Ff8DecArgs a) {
     if constexpr ((LAMD_ABLATE & 16) != 0) return;
     using F = FF8;
     using TL = Tile<F, T, reg_bits8(T), 1>;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    const LdsTab8<256> sk{lds + tile_dwords8(T)};
+    const LdsTab8<256> sk{lds + areas8(NA) * tile_dwords8(T)};
     const LdsTab8<256> ltab{sk.base + LdsTab8<256>::kDwords};  // by log value
+    LdsRing<tile_dwords8(T), areas8(NA)> ring{lds};
     STAMP(0);
     TabStage8<threads8(T), 256> sk_stage, log_stage;
     sk_stage.load(a.sktab);
@@ -171,12 +224,14 @@ __global__ void __launch_bounds__(threads8(T), 4) k_ff8_dec(Ff8DecArgs a) {
     const Cols cl = strip_cols(a.nunits, lane);
     const PieceSpace ps{0, 0, 0};
     const Pyr8Live present{a.present}, needed{a.needed};
+    auto pos = [&](int r) { return TL::piece(0, r, w); };
     typename TL::Reg v;
-    // received pieces: positions [0, R) recovery, [m, m + K) originals (LeopardFF8.cpp:1857-1877)
+    {
+        // received pieces: positions [0, R) recovery, [m, m + K) originals (LeopardFF8.cpp:1857-1877)
+        uint64_t pp[TL::NR];
+        fetch_ptrs(pp, a.ptr, pos);
 #pragma unroll
-    for (int r = 0; r < TL::NR; ++r) {
-        const unsigned p = TL::piece(0, r, w);
-        v[r][0] = present(p, 0) ? gload(a.ptr[p], cl) : 0u;
+        for (int r = 0; r < TL::NR; ++r) v[r][0] = present(pos(r), 0) ? gload(pp[r], cl) : 0u;
     }
     STAMP(1);
     sk_stage.store(sk);
@@ -184,35 +239,33 @@ __global__ void __launch_bounds__(threads8(T), 4) k_ff8_dec(Ff8DecArgs a) {
     __syncthreads();
     STAMP(2);
     // scale by exp(el) (absent pieces stay zero)
-#pragma unroll
-    for (int r = 0; r < TL::NR; ++r) {
-        const unsigned p = TL::piece(0, r, w);
-        if ((LAMD_ABLATE & 128) == 0 && present(p, 0)) F::mul(v[r], v[r], ltab.at(int(el_at(a, p))));
-    }
-#if LAMD_FF8_SGPR_TABS
-    GlobalWindow<FF8> win;
-#else
+    scale_batched<TL>(v, ltab, [&](int r) { return el_at(a, pos(r)); }, [&](int r) { return present(pos(r), 0); });
     LdsSkew8 win{sk};
-#endif
-    win.stage(a.sktab, -1);
-    TL::ifft(v, w, lane, lds, ps, win, present);
-    STAMP(3);
-    TL::derivative_inplace(v, w, lane, lds);
-    STAMP(4);
-    TL::fft(v, w, lane, lds, ps, win, needed);
+    win.stage(nullptr, -1);
+    if constexpr (pipe8(NA)) {
+        TL::ifft_pl(v, w, lane, ring, ps, win, present);
+        STAMP(3);
+        TL::derivative_ring(v, w, lane, ring);
+        STAMP(4);
+        TL::fft_pl(v, w, lane, ring, ps, win, needed);
+    } else {
+        TL::ifft(v, w, lane, lds, ps, win, present);
+        STAMP(3);
+        TL::derivative_inplace(v, w, lane, lds);
+        STAMP(4);
+        TL::fft(v, w, lane, lds, ps, win, needed);
+    }
     STAMP(5);
     TL::pin(v);
-    if (!cl.live) return;
     // lost original at p = m + i: work[i] = z[p] * exp(-el[p])  (LeopardFF8.cpp:1913-1915)
+    uint64_t pp[TL::NR];
+    fetch_ptrs(pp, a.ptr, pos);
+    auto is_needed = [&](int r) { return needed(pos(r), 0); };
+    scale_batched<TL>(v, ltab, [&](int r) { return F::kModulus - el_at(a, pos(r)); }, is_needed);
+    if (!cl.live) return;
 #pragma unroll
-    for (int r = 0; r < TL::NR; ++r) {
-        const unsigned p = TL::piece(0, r, w);
-        if (needed(p, 0)) {
-            uint32_t y[1] = {v[r][0]};
-            if constexpr ((LAMD_ABLATE & 128) == 0) F::mul(y, v[r], ltab.at(int(F::kModulus - el_at(a, p))));
-            gstore(a.ptr[p], cl, y[0]);
-        }
-    }
+    for (int r = 0; r < TL::NR; ++r)
+        if (is_needed(r)) gstore(pp[r], cl, v[r][0]);
     STAMP(6);
 }
 
@@ -228,7 +281,7 @@ struct Once {
     }
 };
 template <class Tag, class KernelFn, class Args>
-hipError_t launch8(KernelFn* fn, unsigned T, const Args& a, size_t lds_dwords, hipStream_t s) {
+hipError_t launch8(KernelFn* fn, unsigned threads, const Args& a, size_t lds_dwords, hipStream_t s) {
     const size_t lds = lds_dwords * 4;
     if (lds > 65536) {
         const hipError_t e = Once<Tag>::set_lds(reinterpret_cast<const void*>(fn), lds);
@@ -236,23 +289,38 @@ hipError_t launch8(KernelFn* fn, unsigned T, const Args& a, size_t lds_dwords, h
     }
     void* params[] = {const_cast<Args*>(&a)};
     const dim3 grid((a.nunits + 63) / 64);
-    return hipLaunchKernel(reinterpret_cast<const void*>(fn), grid, dim3(threads8(int(T))), params, lds, s);
+    return hipLaunchKernel(reinterpret_cast<const void*>(fn), grid, dim3(threads), params, lds, s);
 }
 
-template <int T, bool M>
+template <int T, int RB, bool M, int NA>
 struct EncTag {};
-template <int T>
+template <int T, int NA>
 struct DecTag {};
 
+template <int T, int RB, int NA>
+hipError_t enc_RB(const Ff8EncArgs& a, hipStream_t s) {
+    constexpr size_t lds = areas8(NA) * tile_dwords_for(T, RB) + LdsTab8<256>::kDwords;
+    if (a.nchunks > 1)
+        return launch8<EncTag<T, RB, true, NA>>(&k_ff8_enc<T, RB, true, NA>, threads_for(T, RB), a, lds, s);
+    return launch8<EncTag<T, RB, false, NA>>(&k_ff8_enc<T, RB, false, NA>, threads_for(T, RB), a, lds, s);
+}
 template <int T>
 hipError_t enc_T(const Ff8EncArgs& a, hipStream_t s) {
-    constexpr size_t lds = tile_dwords8(T) + LdsTab8<256>::kDwords;
-    if (a.nchunks > 1) return launch8<EncTag<T, true>>(&k_ff8_enc<T, true>, T, a, lds, s);
-    return launch8<EncTag<T, false>>(&k_ff8_enc<T, false>, T, a, lds, s);
+    // wide form once every CU gets >= 4 strips (256 CUs x 4 x 256 B: 256 KiB pieces)
+    if constexpr (wide_bits8(T) != reg_bits8(T))
+        if (a.nunits >= 65536) return enc_RB<T, wide_bits8(T), 1>(a, s);
+    if (a.nunits > kOneWgPerCuUnits) return enc_RB<T, reg_bits8(T), 1>(a, s);
+    return enc_RB<T, reg_bits8(T), 2>(a, s);
+}
+template <int T, int NA>
+hipError_t dec_NA(const Ff8DecArgs& a, hipStream_t s) {
+    constexpr size_t lds = areas8(NA) * tile_dwords8(T) + 2 * LdsTab8<256>::kDwords;
+    return launch8<DecTag<T, NA>>(&k_ff8_dec<T, NA>, threads8(T), a, lds, s);
 }
 template <int T>
 hipError_t dec_T(const Ff8DecArgs& a, hipStream_t s) {
-    return launch8<DecTag<T>>(&k_ff8_dec<T>, T, a, tile_dwords8(T) + 2 * LdsTab8<256>::kDwords, s);
+    if (a.nunits > kOneWgPerCuUnits) return dec_NA<T, 1>(a, s);
+    return dec_NA<T, 2>(a, s);
 }
 
 }  // namespace

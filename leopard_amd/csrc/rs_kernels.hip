@@ -30,10 +30,7 @@ constexpr int C = kUnitsPerLane;
 // Register bits per lane for a tile of T bits: 8 pieces per lane when that
 // gives at most 16 waves (more waves per SIMD hide the butterfly chains'
 // latency), otherwise 16 pieces (T = 8: 16 waves of 16 pieces).
-#ifndef LAMD_RB7  // experiment hook: register bits for 7-bit tiles
-#define LAMD_RB7 3
-#endif
-constexpr int reg_bits(int T) { return T <= 3 ? T : T == 7 ? LAMD_RB7 : (T - 3 <= 4 ? 3 : T - 4); }
+constexpr int reg_bits(int T) { return T <= 3 ? T : (T - 3 <= 4 ? 3 : T - 4); }
 constexpr int wave_bits(int T) { return T - reg_bits(T); }
 
 // LDS carve-up: the tile transpose area

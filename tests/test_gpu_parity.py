@@ -296,3 +296,47 @@ def test_column_shards_on_device_equal_whole_call(leo, k, r, b, world):
     torch.cuda.synchronize()
     for i in lost:
         assert torch.equal(dwork[i], o[i]), i
+
+
+# ------------------------------------------------- host-memory pipeline --
+
+@pytest.mark.parametrize("k,r,b,loss", [(128, 128, 1 << 18, 128), (100, 30, 64 * 1000, 17), (1000, 200, 1 << 14, 200),
+                                        (9, 1, 1 << 16, 1)])
+def test_host_pipeline_roundtrip(leo, k, r, b, loss):
+    """Host (pageable) buffers large enough to be cut into several column
+    slices (two-slot ring, FF8 on two streams, FF16 on one): encode must match
+    the oracle and the decode of the benchmark loss pattern must rebuild the
+    originals, all in host memory (leopard.h:147-186, 205-234)."""
+    data = ol.pcg_bytes(4, k, k, b)
+    wc = leo.leo_encode_work_count(k, r)
+    work = np.zeros((wc, b), dtype=np.uint8)
+    res = leo.leo_encode(b, k, r, wc, [data[i].ctypes.data for i in range(k)], [work[i].ctypes.data for i in range(wc)])
+    assert res == leo.LeopardResult.Success, leo.last_error()
+    sub = slice(0, 4096)  # the oracle on a column prefix (columns are independent)
+    assert np.array_equal(work[:r, sub], ol.oracle().encode(np.ascontiguousarray(data[:, sub]), r))
+    rec = work[:r].copy()
+    lo, lr = ol.benchmark_losses(k, r, loss, seed=4, trial=k)
+    dwc = leo.leo_decode_work_count(k, r)
+    dwork = np.zeros((dwc, b), dtype=np.uint8)
+    res = leo.leo_decode(b, k, r, dwc, [None if i in lo else data[i].ctypes.data for i in range(k)],
+                         [None if i in lr else rec[i].ctypes.data for i in range(r)],
+                         [dwork[i].ctypes.data for i in range(dwc)])
+    assert res == leo.LeopardResult.Success, leo.last_error()
+    for i in lo:
+        assert np.array_equal(dwork[i], data[i]), i
+
+
+def test_host_edge_paths(leo):
+    """K == 1 and zero-loss host calls are copies (leopard.cpp:143-149, 279-291)."""
+    d = ol.pcg_bytes(6, 0, 1, 640)
+    work = np.zeros((1, 640), dtype=np.uint8)
+    assert leo.leo_encode(640, 1, 1, 1, [d[0].ctypes.data], [work[0].ctypes.data]) == 0
+    assert np.array_equal(work[0], d[0])
+    k, r, b = 20, 5, 192
+    d = ol.pcg_bytes(6, 1, k, b)
+    rec = ol.oracle().encode(d, r)
+    dwc = leo.leo_decode_work_count(k, r)
+    dwork = np.zeros((dwc, b), dtype=np.uint8)
+    assert leo.leo_decode(b, k, r, dwc, [d[i].ctypes.data for i in range(k)], [rec[i].ctypes.data for i in range(r)],
+                          [dwork[i].ctypes.data for i in range(dwc)]) == 0
+    assert np.array_equal(dwork[:k], d)

@@ -4,8 +4,12 @@
 Metric (BASELINE.json): device-resident encode+decode GB/s of input bytes.
 One *step* = one leo_encode of a batch plus one worst-case leo_decode of the
 same batch (every original lost, decoded from the R recovery pieces), both
-called through the drop-in C ABI with device pointers, in async mode on one
-HIP stream.  value = (input bytes K*B per step, summed over ranks) / time.
+called through the drop-in C ABI with device pointers, in async mode.  Step s
+runs on HIP stream s % S (--streams, default 3 objects in flight: a single
+64 KiB-piece call fills each CU with one workgroup, and concurrent objects
+fill the phases where one call waits on memory or barriers); the same steps on
+one stream are reported as "serial".  value = (input bytes K*B per step,
+summed over ranks) / time.
 
 Workload (configs[1]): 128 originals + 128 recovery pieces of 65536 bytes,
 GF(2^8).  Every rank owns its own 64 KiB-per-piece column shard of a larger
@@ -14,9 +18,11 @@ per-GPU work is fixed as N grows -> "scaling": "weak".  To defeat the 256 MiB
 Infinity Cache the step walks over >= 16 distinct buffer sets (> 2x MALL).
 
 Roofline: the dominant kernel is timed alone with HIP events on the stream it
-runs on (back-to-back calls); achieved = algorithmic bytes per launch
-((K_surv + lost) * B for decode, (K + R) * B for encode) / mean
-launch duration, against the 8 TB/s HBM3E peak.
+runs on (back-to-back calls queued behind a spin kernel); achieved =
+algorithmic bytes per launch ((K_surv + lost) * B for decode, (K + R) * B for
+encode) / mean launch duration, against the 8 TB/s HBM3E peak.
+traffic = HBM bytes per launch from the committed rocprofv3 PMC pass
+(tools/pmc_traffic.py), when present for this workload.
 
 cpu_baseline: the reference library compiled from its sources
 (oracle/_ref/libleopard_ref.so, AVX2, single thread -- FF8 has no OpenMP) timed
@@ -41,8 +47,8 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--K", type=int, default=128)
     ap.add_argument("--R", type=int, default=128)
     ap.add_argument("--bytes", type=int, default=65536)
@@ -50,6 +56,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--secondary", action="store_true", help="also time 32768+32768 x 64 KiB (FF16)")
+    ap.add_argument("--no-host", action="store_true", help="skip the host-memory (PCIe-inclusive) rate")
+    ap.add_argument("--streams", type=int, default=3,
+                    help="objects in flight: step s runs on HIP stream s %% S (1 = strictly serial steps)")
     return ap.parse_args()
 
 
@@ -144,33 +153,54 @@ def main():
         if world > 1:
             dist.barrier()
 
-    for s in range(args.warmup):
-        enc(s % sets.n)
-        dec(s % sets.n)
-    barrier()
-    t0 = time.perf_counter()
-    for s in range(args.steps):
-        i = s % sets.n
-        if enc(i) != 0 or dec(i) != 0:
-            raise RuntimeError(leo.last_error())
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    elapsed = max_over_ranks(t1 - t0)
-    if world > 1:
-        barrier()
+    # Objects in flight: step s (encode of buffer set i, then the decode of its
+    # recovery pieces) runs on stream s % S, so up to S independent objects are
+    # coded concurrently -- how a storage node keeps the GPU busy with stripes
+    # whose single calls are too small to fill 256 CUs.  Steps on one stream
+    # stay ordered; buffer sets rotate over >= 16 sets, so concurrent steps
+    # never share buffers.
+    streams = [torch.cuda.Stream(device) for _ in range(max(1, args.streams))]
 
-    # per-kernel launch durations with HIP events on the launch stream
+    def run_steps(nsteps, nstreams):
+        for s in range(nsteps):
+            i = s % sets.n
+            leo.set_stream(streams[s % nstreams].cuda_stream)
+            if enc(i) != 0 or dec(i) != 0:
+                raise RuntimeError(leo.last_error())
+
+    def timed(nstreams):
+        run_steps(args.warmup, nstreams)
+        barrier()
+        t0 = time.perf_counter()
+        run_steps(args.steps, nstreams)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        el = max_over_ranks(t1 - t0)
+        if world > 1:
+            barrier()
+        return el
+
+    elapsed = timed(len(streams))
+    elapsed_serial = timed(1) if len(streams) > 1 else elapsed
+    leo.set_stream(stream.cuda_stream)
+
+    # Per-launch kernel duration with HIP events on the launch stream: a spin
+    # kernel holds the stream while the host enqueues n back-to-back calls (one
+    # kernel each on the FF8 path) between one event pair, so the pair holds
+    # only GPU time; back-to-back kernels start as the previous one ends
+    # (rocprofv3 trace: median gap 0), so time / n is the mean launch duration.
     def time_calls(fn, n=100):
-        ev0 = torch.cuda.Event(enable_timing=True)
-        ev1 = torch.cuda.Event(enable_timing=True)
         for j in range(10):
             fn(j % sets.n)
-        ev0.record(stream)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda._sleep(50_000_000)
+        e0.record(stream)
         for j in range(n):
             fn(j % sets.n)
-        ev1.record(stream)
-        ev1.synchronize()
-        return ev0.elapsed_time(ev1) / 1e3 / n
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / 1e3 / n
 
     t_enc = time_calls(enc)
     t_dec = time_calls(dec)
@@ -182,11 +212,13 @@ def main():
     secondary = None
     if args.secondary and rank == 0:
         secondary = run_secondary(leo, torch, device)
+    host = host_e2e(leo, k, r, nbytes) if rank == 0 and not args.no_host else None
 
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
         cpu = cpu_baseline(k, r, nbytes, args.cpu_seconds)
 
+    traffic = pmc_traffic(dominant[0], k, r, nbytes)
     if rank == 0:
         value = world * in_bytes * args.steps / elapsed / 1e9
         achieved = dominant[1] / dominant[2] / 1e9
@@ -204,18 +236,25 @@ def main():
             "dtype": "u8",
             "data": "synthetic (counter-hash bytes on device)",
             "config": {"workload": f"{k}+{r} x {nbytes} B pieces, GF(2^8), encode + full-loss decode per step, "
-                                   f"device-resident, {sets.n} rotating buffer sets",
+                                   f"device-resident, {sets.n} rotating buffer sets, "
+                                   f"{len(streams)} objects in flight",
                        "original_count": k, "recovery_count": r, "buffer_bytes": nbytes, "losses": k,
                        "field": "FF8" if leo.leo_decode_work_count(k, r) <= 256 else "FF16",
+                       "objects_in_flight": len(streams),
                        "sharding": "64-byte column blocks per rank, no collective"},
+            "serial": {"value": round(world * in_bytes * args.steps / elapsed_serial / 1e9, 3),
+                       "ms_per_step": round(elapsed_serial / args.steps * 1e3, 4),
+                       "note": "same steps, one stream (each step waits for the previous)"},
             "encode_GBps": round(in_bytes / t_enc / 1e9, 3),
             "decode_GBps": round(in_bytes / t_dec / 1e9, 3),
             "encode_us": round(t_enc * 1e6, 3),
             "decode_us": round(t_dec * 1e6, 3),
             "roofline": {"bound": "hbm", "kernel": dominant[0], "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                         "traffic": None, "algorithmic_bytes_per_launch": dominant[1]},
+                         "traffic": traffic.get("bytes"), "traffic_source": traffic.get("source"),
+                         "algorithmic_bytes_per_launch": dominant[1]},
             "cpu_baseline": cpu,
+            "host_e2e": host,
         }
         if secondary:
             out["secondary"] = secondary
@@ -262,6 +301,58 @@ def run_secondary(leo, torch, device):
     del o, ew, dw
     torch.cuda.empty_cache()
     return res
+
+
+def host_e2e(leo, k, r, nbytes, steps=20):
+    """PCIe-inclusive rate: the same encode + full-loss decode step through the
+    C ABI with caller-owned pageable host buffers (the reference's contract).
+    The library stages them through its pinned two-slot ring.  Not `value`."""
+    import numpy as np
+    data = np.frombuffer(np.random.default_rng(7).bytes(k * nbytes), dtype=np.uint8).reshape(k, nbytes)
+    wc, dwc = leo.leo_encode_work_count(k, r), leo.leo_decode_work_count(k, r)
+    work = np.zeros((wc, nbytes), dtype=np.uint8)
+    dwork = np.zeros((dwc, nbytes), dtype=np.uint8)
+    po = [data[i].ctypes.data for i in range(k)]
+    pe = [work[i].ctypes.data for i in range(wc)]
+    pr = [work[i].ctypes.data for i in range(r)]
+    pd = [dwork[i].ctypes.data for i in range(dwc)]
+    lost = [None] * k
+
+    def step():
+        assert leo.leo_encode(nbytes, k, r, wc, po, pe) == 0, leo.last_error()
+        assert leo.leo_decode(nbytes, k, r, dwc, lost, pr, pd) == 0, leo.last_error()
+
+    step()
+    t0 = time.perf_counter()
+    t_enc = 0.0
+    for _ in range(steps):
+        a = time.perf_counter()
+        assert leo.leo_encode(nbytes, k, r, wc, po, pe) == 0, leo.last_error()
+        t_enc += time.perf_counter() - a
+        assert leo.leo_decode(nbytes, k, r, dwc, lost, pr, pd) == 0, leo.last_error()
+    dt = time.perf_counter() - t0
+    ok = bool(np.array_equal(dwork[:k], data))
+    inb = k * nbytes
+    return {"value": round(inb * steps / dt / 1e9, 3), "unit": "GB/s", "encode_GBps": round(inb * steps / t_enc / 1e9, 3),
+            "decode_GBps": round(inb * steps / (dt - t_enc) / 1e9, 3), "roundtrip_ok": ok,
+            "sample": f"{steps} steps, pageable numpy buffers, H2D + kernels + D2H per call"}
+
+
+def pmc_traffic(kernel, k, r, nbytes):
+    """HBM bytes per launch of the dominant kernel from the committed PMC pass
+    (tools/pmc_traffic.py: FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md HBM
+    section), when one exists for this workload; else None."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*", "pmc_traffic.json")), reverse=True):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        e = d.get("workloads", {}).get(f"{k}+{r}x{nbytes}", {}).get(kernel)
+        if e:
+            return {"bytes": e["hbm_bytes_per_launch"], "source": os.path.relpath(path, REPO)}
+    return {}
 
 
 def cpu_baseline(k, r, nbytes, seconds):

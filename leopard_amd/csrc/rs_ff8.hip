@@ -19,6 +19,7 @@
 // accumulated (FFT(sum) = F_low(sum of F_top(chunk IFFTs))).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <mutex>
 
 #include "rs_args.h"
@@ -55,24 +56,23 @@ constexpr int reg_bits8(int T) { return T <= 3 ? T : (T - 3 <= 4 ? 3 : T - 4); }
 constexpr int wide_bits8(int T) { return T == 7 ? 4 : reg_bits8(T); }
 constexpr unsigned threads_for(int T, int RB) { return 64u << (T - RB); }
 constexpr size_t tile_dwords_for(int T, int RB) { return T > RB ? (size_t(1) << T) * 64 : 0; }
-constexpr unsigned threads8(int T) { return threads_for(T, reg_bits8(T)); }
-constexpr size_t tile_dwords8(int T) { return tile_dwords_for(T, reg_bits8(T)); }
+constexpr int wide_dec_bits8(int T) { return T == 8 ? 5 : reg_bits8(T); }
 
-// Pipelined transforms (Tile::ifft_pl / fft_pl: lookahead of tables and
-// predicate words, exchanges through an LdsRing of NA areas) or the plain ones
-// (Tile::ifft / fft, one area), for A/B builds.
+// Transforms: the plain ones (Tile::ifft / fft: one LDS area, two barriers
+// per exchange) by default; LAMD_FF8_PIPE=1 builds the pipelined ones
+// (Tile::ifft_pl / fft_pl: lookahead of tables and predicate words, two
+// exchange areas, one barrier per exchange) for launches of at most one
+// workgroup per CU.  Measured on MI355X, 128+128 pieces: pipelined is 3%
+// faster for one 64 KiB encode on an idle GPU, but its LDS footprint keeps
+// kernels of concurrent calls from sharing a CU (3 calls in flight: 22.6 vs
+// 15.8 us per encode+decode step) and at 1 MiB pieces it is 10-15% slower.
 #ifndef LAMD_FF8_PIPE
-#define LAMD_FF8_PIPE 1
+#define LAMD_FF8_PIPE 0
 #endif
 constexpr bool kPipe8 = LAMD_FF8_PIPE != 0;
 constexpr bool pipe8(int NA) { return kPipe8 && NA == 2; }
 constexpr int areas8(int NA) { return pipe8(NA) ? 2 : 1; }
 
-// By grid size: while a launch has at most one workgroup per CU, the pipelined
-// transforms with two exchange areas (one barrier per exchange); for larger
-// launches the plain transforms with one area, whose smaller LDS and register
-// footprint fits more workgroups per CU (measured at 1 MiB pieces: encode 78
-// vs 87 us, decode 195 vs 226 us; at 64 KiB the pipelined encode is 3% faster).
 constexpr uint32_t kOneWgPerCuUnits = 256 * 64;  // 256 CUs x one 64-dword strip
 
 // Piece pointers of the NR pieces a lane holds, fetched as one batch of scalar
@@ -207,17 +207,17 @@ LDEV void scale_batched(typename TL::Reg& v, const LdsTab8<256>& ltab, LogFn log
     });
 }
 
-template <int T, int NA>
-__global__ void __launch_bounds__(threads8(T), 4) k_ff8_dec(Ff8DecArgs a) {
+template <int T, int RB, int NA>
+__global__ void __launch_bounds__(threads_for(T, RB), 4) k_ff8_dec(Ff8DecArgs a) {
     if constexpr ((LAMD_ABLATE & 16) != 0) return;
     using F = FF8;
-    using TL = Tile<F, T, reg_bits8(T), 1>;
+    using TL = Tile<F, T, RB, 1>;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    const LdsTab8<256> sk{lds + areas8(NA) * tile_dwords8(T)};
+    const LdsTab8<256> sk{lds + areas8(NA) * tile_dwords_for(T, RB)};
     const LdsTab8<256> ltab{sk.base + LdsTab8<256>::kDwords};  // by log value
-    LdsRing<tile_dwords8(T), areas8(NA)> ring{lds};
+    LdsRing<tile_dwords_for(T, RB), areas8(NA)> ring{lds};
     STAMP(0);
-    TabStage8<threads8(T), 256> sk_stage, log_stage;
+    TabStage8<threads_for(T, RB), 256> sk_stage, log_stage;
     sk_stage.load(a.sktab);
     log_stage.load(a.tabs);
     const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -294,8 +294,18 @@ hipError_t launch8(KernelFn* fn, unsigned threads, const Args& a, size_t lds_dwo
 
 template <int T, int RB, bool M, int NA>
 struct EncTag {};
-template <int T, int NA>
+template <int T, int RB, int NA>
 struct DecTag {};
+
+// Launch shape overrides for experiments (LEO_AMD_FF8_WIDE=1: the wide
+// register forms at every size); read once.
+bool force_wide() {
+    static const bool v = [] {
+        const char* e = std::getenv("LEO_AMD_FF8_WIDE");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
 
 template <int T, int RB, int NA>
 hipError_t enc_RB(const Ff8EncArgs& a, hipStream_t s) {
@@ -308,19 +318,23 @@ template <int T>
 hipError_t enc_T(const Ff8EncArgs& a, hipStream_t s) {
     // wide form once every CU gets >= 4 strips (256 CUs x 4 x 256 B: 256 KiB pieces)
     if constexpr (wide_bits8(T) != reg_bits8(T))
-        if (a.nunits >= 65536) return enc_RB<T, wide_bits8(T), 1>(a, s);
-    if (a.nunits > kOneWgPerCuUnits) return enc_RB<T, reg_bits8(T), 1>(a, s);
-    return enc_RB<T, reg_bits8(T), 2>(a, s);
+        if (a.nunits >= 65536 || force_wide()) return enc_RB<T, wide_bits8(T), 1>(a, s);
+    if constexpr (kPipe8)
+        if (a.nunits <= kOneWgPerCuUnits) return enc_RB<T, reg_bits8(T), 2>(a, s);
+    return enc_RB<T, reg_bits8(T), 1>(a, s);
 }
-template <int T, int NA>
-hipError_t dec_NA(const Ff8DecArgs& a, hipStream_t s) {
-    constexpr size_t lds = areas8(NA) * tile_dwords8(T) + 2 * LdsTab8<256>::kDwords;
-    return launch8<DecTag<T, NA>>(&k_ff8_dec<T, NA>, threads8(T), a, lds, s);
+template <int T, int RB, int NA>
+hipError_t dec_RB(const Ff8DecArgs& a, hipStream_t s) {
+    constexpr size_t lds = areas8(NA) * tile_dwords_for(T, RB) + 2 * LdsTab8<256>::kDwords;
+    return launch8<DecTag<T, RB, NA>>(&k_ff8_dec<T, RB, NA>, threads_for(T, RB), a, lds, s);
 }
 template <int T>
 hipError_t dec_T(const Ff8DecArgs& a, hipStream_t s) {
-    if (a.nunits > kOneWgPerCuUnits) return dec_NA<T, 1>(a, s);
-    return dec_NA<T, 2>(a, s);
+    if constexpr (wide_dec_bits8(T) != reg_bits8(T))
+        if (force_wide()) return dec_RB<T, wide_dec_bits8(T), 1>(a, s);
+    if constexpr (kPipe8)
+        if (a.nunits <= kOneWgPerCuUnits) return dec_RB<T, reg_bits8(T), 2>(a, s);
+    return dec_RB<T, reg_bits8(T), 1>(a, s);
 }
 
 }  // namespace

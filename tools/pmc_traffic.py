@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""HBM traffic per launch of the encode / decode kernels from rocprofv3 PMC passes.
+
+GPU box:  KB_ARGS="128 128 65536" bash tools/pmc.sh FETCH_SIZE WRITE_SIZE
+          python3 tools/pmc_traffic.py 128 128 65536 gpurun_out/pmc1 gpurun_out/pmc2 > profiles/<round>/pmc_traffic.json
+
+FETCH_SIZE and WRITE_SIZE are KiB per dispatch.  On gfx950 FETCH_SIZE counts
+half the bytes of coalesced streaming reads (MI355X_MICROARCH.md, HBM section),
+so HBM bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.  For these kernels the x2
+calibration checks out against the algorithmic read bytes (one dword per lane
+per piece, every piece read once).  bench.py reports it as roofline.traffic."""
+import csv
+import glob
+import json
+import re
+import sys
+from collections import defaultdict
+
+
+def kernel_kind(name):
+    if "k_ff8_enc" in name or "k_enc" in name:
+        return "encode"
+    if "k_ff8_dec" in name or "k_dec" in name:
+        return "decode"
+    return None
+
+
+def main():
+    k, r, b = (int(x) for x in sys.argv[1:4])
+    dirs = sys.argv[4:]
+    vals = defaultdict(lambda: defaultdict(list))
+    names = {}
+    for d in dirs:
+        for f in glob.glob(d.rstrip("/") + "/**/*counter_collection.csv", recursive=True):
+            for row in csv.DictReader(open(f)):
+                kind = kernel_kind(row["Kernel_Name"])
+                if kind is None:
+                    continue
+                names[kind] = re.sub(r"^.*::(k_\w+<[^>]*>).*$", r"\1", row["Kernel_Name"])
+                vals[kind][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    out = {}
+    for kind, cs in vals.items():
+        fetch = sum(cs["FETCH_SIZE"]) / len(cs["FETCH_SIZE"])
+        write = sum(cs["WRITE_SIZE"]) / len(cs["WRITE_SIZE"])
+        out[kind] = {"kernel": names[kind], "FETCH_SIZE_KiB": round(fetch, 1), "WRITE_SIZE_KiB": round(write, 1),
+                     "dispatches": len(cs["FETCH_SIZE"]),
+                     "hbm_bytes_per_launch": int((2 * fetch + write) * 1024),
+                     "algorithmic_bytes_per_launch": (k + r) * b}
+    print(json.dumps({"workloads": {f"{k}+{r}x{b}": out},
+                      "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes; (2*FETCH+WRITE) KiB"},
+                     indent=1))
+
+
+if __name__ == "__main__":
+    main()

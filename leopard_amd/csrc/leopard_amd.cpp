@@ -271,8 +271,16 @@ struct MapBuilder {
 
 // Column range processed per pass sequence of the multi-pass FF16 kernels:
 // keep the intermediates (pieces x slice) around the 256 MiB Infinity Cache.
+uint64_t mall_budget() {
+    static const uint64_t v = [] {
+        const char* e = std::getenv("LEO_AMD_SLICE_MB");  // tuning experiments
+        const long mb = e ? std::atol(e) : 3072;
+        return uint64_t(std::max(1L, mb)) << 20;
+    }();
+    return v;
+}
 uint64_t mall_slice(uint64_t bytes, uint64_t slab_pieces) {
-    const uint64_t budget = 160ull << 20;
+    const uint64_t budget = mall_budget();
     uint64_t slice = budget / std::max<uint64_t>(slab_pieces, 1);
     slice = std::max<uint64_t>(slice / 512 * 512, 512);  // whole FF16 tiles (64 units x 8 B)
     return std::min(slice, bytes);

@@ -34,6 +34,9 @@
 #ifndef LAMD_ABLATE
 #define LAMD_ABLATE 0
 #endif
+#ifndef LAMD_FF16_PREFETCH
+#define LAMD_FF16_PREFETCH 0
+#endif
 
 namespace lamd {
 
@@ -508,6 +511,7 @@ struct Tile {
                 __builtin_amdgcn_sched_barrier(0);  // keep the next batch's tables below this one
             });
         } else {
+#if LAMD_FF16_PREFETCH
             // FF16 (20-dword tables in SGPRs): software pipeline, two tables live.
             typename F::Tab next = table(0);
             static_for<0, NG>([&](auto GI) {
@@ -518,6 +522,14 @@ struct Tile {
                 if (live(g)) group(g, t);
                 __builtin_amdgcn_sched_barrier(0);
             });
+#else
+            // FF16 (20-dword tables in SGPRs): one table live at a time, read
+            // inside the live branch (a second live table spilled SGPRs).
+            static_for<0, NG>([&](auto GI) {
+                constexpr int g = decltype(GI)::value * 2 * half;
+                if (live(g)) group(g, table(g));
+            });
+#endif
         }
     }
 

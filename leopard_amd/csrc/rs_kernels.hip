@@ -228,12 +228,13 @@ struct State16 {
     LDEV FF16::Tab table(unsigned lm) const { return FF16::tab(tabs, lm); }
 };
 
-// Received piece at codeword position p, scaled by exp(el[p]); zero if absent.
-// Positions: [0, m) recovery (only [0, R) exist), [m, m+K) originals
+// Received piece at codeword position p (to be scaled by exp(el[p])); zero if
+// absent.  Positions: [0, m) recovery (only [0, R) exist), [m, m+K) originals
 // (LeopardFF8.cpp:1857-1877).  Branch-free on the vector side: an absent piece
-// reads the zero page at unit 0 through the all-zero multiply table.
+// reads the zero page at unit 0 and is scaled through the all-zero table.
+// Returns the log of the scale factor.
 template <class F, class St>
-LDEV void load_received(uint32_t* x, const DecArgs& a, const St& st, unsigned p, uint64_t q) {
+LDEV unsigned load_received(uint32_t* x, const DecArgs& a, const St& st, unsigned p, uint64_t q) {
     const uint8_t* src = a.zeros;
     unsigned lm = F::kModulus + 1;  // the zero table
     uint64_t qq = 0;
@@ -241,11 +242,8 @@ LDEV void load_received(uint32_t* x, const DecArgs& a, const St& st, unsigned p,
         if (p < a.R) { src = a.rec.ptr(p); lm = st.loc(p); qq = q; }
         else if (p >= a.m && p < a.m + a.K) { src = a.orig.ptr(p - a.m); lm = st.loc(p); qq = q; }
     }
-    uint32_t y[C * F::kDw];
-    load_units<F, C>(y, src, qq);
-    const typename F::Tab t = st.table(lm);
-#pragma unroll
-    for (int u = 0; u < C; ++u) F::mul(&x[u * F::kDw], &y[u * F::kDw], t);
+    load_units<F, C>(x, src, qq);
+    return lm;
 }
 
 // Lost original at position p = m + i: work[i] = z[p] * exp(-el[p])  (LeopardFF8.cpp:1913-1915).
@@ -274,9 +272,16 @@ __global__ void __launch_bounds__(64 << wave_bits(kLoBits), 4) k_dec_lo(DecArgs 
     const PieceSpace ps{0, 0, blockIdx.y << T};
     const State16 st{a.erased_dev, a.el, a.tabs};
     typename TL::Reg v;
+    // every piece load in flight first, then the scale multiplies (one table
+    // live at a time)
+    unsigned lm[TL::NR];
+#pragma unroll
+    for (int r = 0; r < TL::NR; ++r) lm[r] = load_received<F>(v[r], a, st, ps.global(TL::piece(0, r, w)), ql);
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) {
-        load_received<F>(v[r], a, st, ps.global(TL::piece(0, r, w)), ql);
+        const typename F::Tab t = st.table(lm[r]);
+#pragma unroll
+        for (int u = 0; u < C; ++u) F::mul(&v[r][u * F::kDw], &v[r][u * F::kDw], t);
         __builtin_amdgcn_sched_barrier(0);
     }
     win.stage(a.sktab, -1);

@@ -22,7 +22,8 @@ def run(k, r, b, sets=16, n=100, warm=int(os.environ.get('KB_WARM', '300'))):
         ew = torch.zeros((ewc, b), dtype=torch.uint8, device="cuda")
         dw = torch.zeros((dwc, b), dtype=torch.uint8, device="cuda")
         S.append((o, ew, dw, (VP * k)(*[o[i].data_ptr() for i in range(k)]),
-                  (VP * ewc)(*[ew[i].data_ptr() for i in range(ewc)]), (VP * k)(),
+                  (VP * ewc)(*[ew[i].data_ptr() for i in range(ewc)]),
+                  (VP * k)(*([None] * min(k, r) + [o[i].data_ptr() for i in range(min(k, r), k)])),
                   (VP * r)(*[ew[i].data_ptr() for i in range(r)]), (VP * dwc)(*[dw[i].data_ptr() for i in range(dwc)])))
     enc = lambda i: lib.leo_encode(b, k, r, ewc, S[i][3], S[i][4])
     dec = lambda i: lib.leo_decode(b, k, r, dwc, S[i][5], S[i][6], S[i][7])
@@ -31,7 +32,8 @@ def run(k, r, b, sets=16, n=100, warm=int(os.environ.get('KB_WARM', '300'))):
     torch.cuda.synchronize()
     rc = dec(0)
     torch.cuda.synchronize()
-    ok = rc == 0 and torch.equal(S[0][2][:k], S[0][0])
+    lost = min(k, r)  # the first min(K, R) originals are lost
+    ok = rc == 0 and torch.equal(S[0][2][:lost], S[0][0][:lost])
     st = torch.cuda.current_stream()
 
     def t(fn):

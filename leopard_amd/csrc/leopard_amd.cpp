@@ -440,19 +440,29 @@ LeopardResult decode_device8(Call& c, uint64_t bytes, uint64_t off, unsigned K, 
     };
     auto addr = [&](const void* p) { return uint64_t(reinterpret_cast<uintptr_t>(p)) + off; };
     for (unsigned i = 0; i < R; ++i)
-        if (rec[i]) {
-            a.ptr[i] = addr(rec[i]);
-            mark(a.present, i);
-        }
-    for (unsigned i = 0; i < K; ++i) {
-        if (orig[i]) {
-            a.ptr[m + i] = addr(orig[i]);
-            mark(a.present, m + i);
-        } else {
-            a.ptr[m + i] = addr(work[i]);  // lost: its slot carries the output
-            mark(a.needed, m + i);
-        }
+        if (rec[i]) a.ptr[i] = addr(rec[i]);
+    for (unsigned i = 0; i < K; ++i)
+        a.ptr[m + i] = addr(orig[i] ? orig[i] : work[i]);  // lost: its slot carries the output
+    // The pyramids depend only on (K, R, erasure pattern); the last pattern is
+    // cached per thread (repeated patterns are the common case).
+    struct PyrCache {
+        unsigned K = 0, R = 0;
+        uint32_t erased[8] = {~0u};
+        uint32_t present[kPyr8Words], needed[kPyr8Words];
+    };
+    thread_local PyrCache pc;
+    if (pc.K != K || pc.R != R || std::memcmp(pc.erased, erased.data(), sizeof(pc.erased)) != 0) {
+        std::memset(pc.present, 0, sizeof(pc.present));
+        std::memset(pc.needed, 0, sizeof(pc.needed));
+        for (unsigned i = 0; i < R; ++i)
+            if (rec[i]) mark(pc.present, i);
+        for (unsigned i = 0; i < K; ++i) mark(orig[i] ? pc.present : pc.needed, m + i);
+        pc.K = K;
+        pc.R = R;
+        std::memcpy(pc.erased, erased.data(), sizeof(pc.erased));
     }
+    std::memcpy(a.present, pc.present, sizeof(a.present));
+    std::memcpy(a.needed, pc.needed, sizeof(a.needed));
     error_locator8(erased, a.el);
     a.sktab = c.t->sktab8;
     a.tabs = c.t->tab8;
@@ -512,7 +522,7 @@ LeopardResult decode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
             if (rec[i]) mark(pyr_present, i);
         for (unsigned i = 0; i < K; ++i) mark(orig[i] ? pyr_present : pyr_needed, m + i);
     }
-    const uint64_t slab_pieces = 3ull * n;
+    const uint64_t slab_pieces = 2ull * n;  // U (pass 1 -> 2, 3) and A (pass 2 -> 3)
     const uint64_t slice = mall_slice(bytes, slab_pieces);
     const size_t table_bytes = (mb.bytes() + 255) / 256 * 256;
     const size_t off_bitmap = table_bytes;
@@ -549,8 +559,7 @@ LeopardResult decode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
     a.nlo = (m + K + (1u << kLoBits) - 1) >> kLoBits;
 
     uint8_t* A = c.ws->dbuf + off_slab;
-    uint8_t* B = A + uint64_t(n) * slice;
-    uint8_t* Uu = B + uint64_t(n) * slice;
+    uint8_t* Uu = A + uint64_t(n) * slice;
     for (uint64_t pos = 0; pos < bytes; pos += slice) {
         const uint64_t len = std::min(slice, bytes - pos);
         DecArgs b = a;
@@ -562,10 +571,9 @@ LeopardResult decode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
         HIP_OK(launch_decode_lo(b, c.s), "decode pass 1");
         b.a_in = PieceMap{nullptr, Uu, slice, 0};
         b.a_out = PieceMap{nullptr, A, slice, 0};
-        b.b_out = PieceMap{nullptr, B, slice, 0};
         HIP_OK(launch_decode_hi(b, c.s), "decode pass 2");
         b.a_in = PieceMap{nullptr, A, slice, 0};
-        b.b_in = PieceMap{nullptr, B, slice, 0};
+        b.b_in = PieceMap{nullptr, Uu, slice, 0};
         HIP_OK(launch_decode_fin(b, c.s), "decode pass 3");
     }
     return Leopard_Success;

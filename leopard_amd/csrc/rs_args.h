@@ -31,7 +31,7 @@ struct EncArgs {
 
 struct DecArgs {
     PieceMap orig, rec, out;
-    PieceMap a_in, b_in, a_out, b_out;  // multi-pass intermediates
+    PieceMap a_in, b_in, a_out;  // multi-pass intermediates (FF16 decode: U, A)
     const uint32_t* sktab;
     const uint32_t* tabs;
     const uint8_t* zeros;

@@ -799,6 +799,55 @@ struct Tile {
         });
     }
 
+    // The decoder's top IFFT layer, the formal derivative and the top FFT
+    // layer collapse: both top layers use the same skew c (offset -1, group 0),
+    // so with (x, y) a pair across the top bit, F_top (I + D_top) I_top maps
+    // (x, y) -> (y, x) (the multiplies cancel: y1 = x ^ y, x1 = x ^ c*y1,
+    // x2 = x1 ^ y1, x3 = x2 ^ c*y1 = y, y3 = y1 ^ x3 = x), F_top I_top = I, and
+    // the lower-bit terms D_low commute with the single-skew top layers:
+    //   F (I + D) I = F_low (swap_top + D_low) I_low.
+    // This computes v <- swap_top(v) + D_low(v) in layout kLast after an IFFT
+    // without its top layer; the FFT then skips its top layer as well.
+    // `area`: LDS for the wave-bit terms; pre_barrier: wait for earlier reads.
+    LDEV static void derivative_swaptop(Reg& v, unsigned w, unsigned lane, uint32_t* area, bool pre_barrier) {
+        if constexpr ((LAMD_ABLATE & 64) != 0) return;
+        constexpr int H = NR / 2;  // register bit of the top tile bit (kLast holds the top R bits)
+        if constexpr (T > R) {
+            if (pre_barrier) __syncthreads();
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                uint32_t* p = area + (size_t(piece(kLast, r, w)) * 64 + lane) * U;
+#pragma unroll
+                for (int k = 0; k < U; ++k) p[k] = v[r][k];
+            }
+        }
+        Reg o;
+        copy(o, v);
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+#pragma unroll
+            for (int k = 0; k < U; ++k) v[r][k] = o[r ^ H][k];
+#pragma unroll
+            for (int b = 0; b + 1 < R; ++b)
+                if (!(r & (1 << b)))
+#pragma unroll
+                    for (int k = 0; k < U; ++k) v[r][k] ^= o[r | (1 << b)][k];
+        }
+        if constexpr (T > R) {
+            __syncthreads();
+            for (int b = 0; b < T - R; ++b) {
+                if (w & (1u << b)) continue;  // wave-uniform
+                const unsigned w2 = w | (1u << b);
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    const uint32_t* p = area + (size_t(piece(kLast, r, w2)) * 64 + lane) * U;
+#pragma unroll
+                    for (int k = 0; k < U; ++k) v[r][k] ^= p[k];
+                }
+            }
+        }
+    }
+
     // v = (I + D) v in place: the derivative of a transform that fits the tile
     // (layout kLast).  Register bits: ascending r reads v[r | 2^b] before it is
     // modified; wave bits: gathered from an LDS copy of the original v.

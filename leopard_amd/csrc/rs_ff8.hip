@@ -242,18 +242,20 @@ __global__ void __launch_bounds__(threads_for(T, RB), 4) k_ff8_dec(Ff8DecArgs a)
     scale_batched<TL>(v, ltab, [&](int r) { return el_at(a, pos(r)); }, [&](int r) { return present(pos(r), 0); });
     LdsSkew8 win{sk};
     win.stage(nullptr, -1);
+    // IFFT and FFT without their top layers around swap_top + D_low (see
+    // Tile::derivative_swaptop): the same map as IFFT, (I + D), FFT
     if constexpr (pipe8(NA)) {
-        TL::ifft_pl(v, w, lane, ring, ps, win, present);
+        TL::template ifft_pl<true>(v, w, lane, ring, ps, win, present);
         STAMP(3);
-        TL::derivative_ring(v, w, lane, ring);
+        TL::derivative_swaptop(v, w, lane, ring.next(), decltype(ring)::kPreBarrier);
         STAMP(4);
-        TL::fft_pl(v, w, lane, ring, ps, win, needed);
+        TL::template fft_pl<true>(v, w, lane, ring, ps, win, needed);
     } else {
-        TL::ifft(v, w, lane, lds, ps, win, present);
+        TL::template ifft<true>(v, w, lane, lds, ps, win, present);
         STAMP(3);
-        TL::derivative_inplace(v, w, lane, lds);
+        TL::derivative_swaptop(v, w, lane, lds, true);
         STAMP(4);
-        TL::fft(v, w, lane, lds, ps, win, needed);
+        TL::template fft<true>(v, w, lane, lds, ps, win, needed);
     }
     STAMP(5);
     TL::pin(v);

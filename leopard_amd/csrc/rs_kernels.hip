@@ -291,7 +291,10 @@ __global__ void __launch_bounds__(64 << wave_bits(kLoBits), 4) k_dec_lo(DecArgs 
     for (int r = 0; r < TL::NR; ++r) store_units<F, C>(a.a_out.ptr(ps.global(TL::piece(TL::kLast, r, w))), q0, v[r]);
 }
 
-// pass 2: IFFT over the high bits, a = (I + D_hi) v, write F_hi(a), F_hi(v)
+// pass 2: A = F_hi (I + D_hi) I_hi U over the high bits, computed as
+// F_hi' (swap_top + D_hi') I_hi' U without the top layers (Tile::derivative_swaptop).
+// The other term of the split derivative needs F_hi(I_hi U) = U, which pass 3
+// reads straight from pass 1's slab.
 template <class F, int T>
 __global__ void __launch_bounds__(64 << wave_bits(T), 4) k_dec_hi(DecArgs a) {
     using TL = Tile<F, T, reg_bits(T), C>;
@@ -302,27 +305,23 @@ __global__ void __launch_bounds__(64 << wave_bits(T), 4) k_dec_hi(DecArgs a) {
     const bool live = q0 < a.nunits;
     const uint64_t ql = live ? q0 : a.nunits - C;
     const PieceSpace ps{blockIdx.y, kLoBits, 0};
-    typename TL::Reg v, d;
+    typename TL::Reg v;
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) {
         const unsigned tp = TL::piece(0, r, w);
         load_or_zero<F>(v[r], a.a_in, tp < a.nlo, ps.global(tp), a.zeros, ql);
     }
     win.stage(a.sktab, -1);
-    TL::ifft(v, w, lane, lds, ps, win, Pyr16Live{a.present_pyr});
-    TL::copy(d, v);
-    TL::derivative_add(d, v, w, lane, lds);
-    TL::fft(d, w, lane, lds, ps, win, Pyr16Live{a.needed_pyr});
+    TL::template ifft<true>(v, w, lane, lds, ps, win, Pyr16Live{a.present_pyr});
+    TL::derivative_swaptop(v, w, lane, lds, true);
+    TL::template fft<true>(v, w, lane, lds, ps, win, Pyr16Live{a.needed_pyr});
     if (live)
 #pragma unroll
-        for (int r = 0; r < TL::NR; ++r) store_units<F, C>(a.a_out.ptr(ps.global(TL::piece(0, r, w))), q0, d[r]);
-    TL::fft(v, w, lane, lds, ps, win, Pyr16Live{a.needed_pyr});
-    if (live)
-#pragma unroll
-        for (int r = 0; r < TL::NR; ++r) store_units<F, C>(a.b_out.ptr(ps.global(TL::piece(0, r, w))), q0, v[r]);
+        for (int r = 0; r < TL::NR; ++r) store_units<F, C>(a.a_out.ptr(ps.global(TL::piece(0, r, w))), q0, v[r]);
 }
 
-// pass 3: z = A + D_lo(V), FFT over the low bits, reveal lost originals
+// pass 3: z = A + D_lo(U), FFT over the low bits, reveal lost originals (U of
+// a low tile without received data is zero and was never written)
 template <class F>
 __global__ void __launch_bounds__(64 << wave_bits(kLoBits), 4) k_dec_fin(DecArgs a) {
     constexpr int T = kLoBits;
@@ -345,7 +344,7 @@ __global__ void __launch_bounds__(64 << wave_bits(kLoBits), 4) k_dec_fin(DecArgs
     for (int r = 0; r < TL::NR; ++r) {
         const unsigned g = ps.global(TL::piece(TL::kLast, r, w));
         load_units<F, C>(z[r], a.a_in.ptr(g), ql);
-        load_units<F, C>(v[r], a.b_in.ptr(g), ql);
+        load_or_zero<F>(v[r], a.b_in, blockIdx.y < a.nlo, g, a.zeros, ql);
     }
     win.stage(a.sktab, -1);
     TL::derivative_add(z, v, w, lane, lds);

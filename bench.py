@@ -55,7 +55,8 @@ def parse():
     ap.add_argument("--sets", type=int, default=0, help="buffer sets rotated (0 = enough for >512 MiB)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--secondary", action="store_true", help="also time 32768+32768 x 64 KiB (FF16)")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the GF(2^16) configs (32768+32768 and 1000+200 x 64 KiB)")
     ap.add_argument("--no-host", action="store_true", help="skip the host-memory (PCIe-inclusive) rate")
     ap.add_argument("--streams", type=int, default=3,
                     help="objects in flight: step s runs on HIP stream s %% S (1 = strictly serial steps)")
@@ -210,8 +211,9 @@ def main():
     dominant = ("decode", algo_dec, t_dec) if t_dec >= t_enc else ("encode", algo_enc, t_enc)
 
     secondary = None
-    if args.secondary and rank == 0:
-        secondary = run_secondary(leo, torch, device)
+    if not args.no_secondary and rank == 0:
+        secondary = [run_secondary(leo, torch, device, kk, rr, ll) for kk, rr, ll in
+                     ((32768, 32768, 32768), (1000, 200, 200))]
     host = host_e2e(leo, k, r, nbytes) if rank == 0 and not args.no_host else None
 
     cpu = None
@@ -263,24 +265,30 @@ def main():
         dist.destroy_process_group()
 
 
-def run_secondary(leo, torch, device):
-    """32768+32768 x 64 KiB (FF16, BASELINE configs[3]) -- few steps."""
-    k = r = 32768
+def run_secondary(leo, torch, device, k, r, loss):
+    """GF(2^16) configs of BASELINE.json (configs[3], configs[2]) at 64 KiB:
+    encode, then decode with `loss` originals lost (the benchmark's
+    ShuffleDeck16 pattern, tests/benchmark.cpp:440-467) -- a few calls each."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_lib as ol
     nbytes = 65536
     lib = leo.lib
     VP = ctypes.c_void_p
     o = hash_fill_cuda(torch, 7, k, nbytes, device)
     ew = torch.empty((leo.leo_encode_work_count(k, r), nbytes), dtype=torch.uint8, device=device)
     dw = torch.empty((leo.leo_decode_work_count(k, r), nbytes), dtype=torch.uint8, device=device)
+    lo, lr = ol.benchmark_losses(k, r, loss, seed=2, trial=0)
+    los, lrs = set(lo), set(lr)
     po = (VP * k)(*[o[i].data_ptr() for i in range(k)])
     pe = (VP * ew.shape[0])(*[ew[i].data_ptr() for i in range(ew.shape[0])])
-    pn = (VP * k)()
-    pr = (VP * r)(*[ew[i].data_ptr() for i in range(r)])
+    pn = (VP * k)(*[None if i in los else o[i].data_ptr() for i in range(k)])
+    pr = (VP * r)(*[None if i in lrs else ew[i].data_ptr() for i in range(r)])
     pd = (VP * dw.shape[0])(*[dw[i].data_ptr() for i in range(dw.shape[0])])
     s = torch.cuda.current_stream(device)
+    leo.set_stream(s.cuda_stream)
 
     def t(fn, n=3):
-        fn()
+        assert fn() == 0, leo.last_error()
         s.synchronize()
         a = torch.cuda.Event(enable_timing=True)
         b = torch.cuda.Event(enable_timing=True)
@@ -293,11 +301,12 @@ def run_secondary(leo, torch, device):
 
     te = t(lambda: lib.leo_encode(nbytes, k, r, ew.shape[0], po, pe))
     td = t(lambda: lib.leo_decode(nbytes, k, r, dw.shape[0], pn, pr, pd))
-    ok = torch.equal(dw[:k], o)
+    idx = torch.tensor(lo, device=device)
+    ok = bool(torch.equal(dw.index_select(0, idx), o.index_select(0, idx)))
     inb = k * nbytes
-    res = {"workload": "32768+32768 x 65536 B, GF(2^16), full loss", "encode_GBps": round(inb / te / 1e9, 3),
+    res = {"workload": f"{k}+{r} x {nbytes} B, GF(2^16), {loss} originals lost", "encode_GBps": round(inb / te / 1e9, 3),
            "decode_GBps": round(inb / td / 1e9, 3), "encode_decode_GBps": round(inb / (te + td) / 1e9, 3),
-           "encode_ms": round(te * 1e3, 3), "decode_ms": round(td * 1e3, 3), "roundtrip_ok": bool(ok)}
+           "encode_ms": round(te * 1e3, 3), "decode_ms": round(td * 1e3, 3), "roundtrip_ok": ok}
     del o, ew, dw
     torch.cuda.empty_cache()
     return res

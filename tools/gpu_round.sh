@@ -10,7 +10,7 @@ OUT=${OUT:-gpurun_out/round}
 rm -rf $OUT; mkdir -p $OUT
 timeout -k 10 600 python3 bench.py ${BENCH_ARGS:-} > $OUT/bench.json 2> $OUT/bench.err || { tail -30 $OUT/bench.err; exit 1; }
 cat $OUT/bench.json
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-host --streams 1 ${BENCH_ARGS:-} > $OUT/prof_bench.json 2> $OUT/prof.err || { tail -20 $OUT/prof.err; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-host --no-secondary --streams 1 ${BENCH_ARGS:-} > $OUT/prof_bench.json 2> $OUT/prof.err || { tail -20 $OUT/prof.err; exit 1; }
 cat $OUT/prof_bench.json
 find $OUT/prof -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
 KB_ARGS="${PMC_ARGS:-128 128 65536}" bash tools/pmc.sh FETCH_SIZE WRITE_SIZE || exit 1

@@ -171,4 +171,16 @@ void build_fused_top_tables8(const GaloisField& f, const std::vector<uint32_t>& 
     }
 }
 
+void build_fused_top_logs16(const GaloisField& f, std::vector<uint32_t>& out) {
+    out.assign(kFused16Entries, f.order());  // default: the all-zero table
+    auto element = [&](unsigned i) { return f.skew[i] == f.modulus() ? 0u : unsigned(f.exp_of[f.skew[i]]); };
+    for (unsigned T = 1; T <= 15; ++T) {
+        const unsigned m = 1u << T;
+        for (unsigned c = 0; c + 1 < f.order() / m; ++c) {
+            const unsigned e = element(m - 1 + c * m + m / 2) ^ element(m / 2 - 1);
+            out[fused16_base(T) + c] = e == 0 ? f.order() : f.log_of[e];
+        }
+    }
+}
+
 }  // namespace lamd

@@ -85,4 +85,11 @@ constexpr unsigned kFused8Entries = 7 * 256;
 void build_fused_top_tables8(const GaloisField& f, const std::vector<uint32_t>& perm_tables,
                              std::vector<uint32_t>& out);
 
+// FF16 encoders: the same fused top layer as a table index (log value, or
+// order() for the all-zero table) per (T, chunk c) at fused16_base(T) + c,
+// T = 1..15 (65536 >> T chunks each); the kernels read tab16[index].
+constexpr unsigned kFused16Entries = 65536;
+constexpr unsigned fused16_base(unsigned T) { return 65536u - (131072u >> T); }
+void build_fused_top_logs16(const GaloisField& f, std::vector<uint32_t>& out);
+
 }  // namespace lamd

@@ -61,6 +61,7 @@ struct DeviceTables {
     uint32_t* sktab8 = nullptr;   // skew-indexed butterfly tables, 256 x 8 dwords
     uint32_t* sktab16 = nullptr;  // 65536 x 24 dwords
     uint32_t* fused8 = nullptr;  // fused top-layer tables of the FF8 encoder
+    uint32_t* fused16 = nullptr;  // fused top-layer table indices of the FF16 encoders
     uint32_t* walsh8 = nullptr;
     uint32_t* walsh16 = nullptr;
     uint8_t* zeros = nullptr;   // zero page
@@ -71,7 +72,7 @@ std::mutex g_mu;
 bool g_initialized = false;
 int g_device_count = 0;
 std::vector<DeviceTables> g_dev;
-std::vector<uint32_t> g_h_tab8, g_h_tab16, g_h_sktab8, g_h_sktab16, g_h_fused8, g_h_walsh8, g_h_walsh16;
+std::vector<uint32_t> g_h_tab8, g_h_tab16, g_h_sktab8, g_h_sktab16, g_h_fused8, g_h_fused16, g_h_walsh8, g_h_walsh16;
 
 template <class T>
 hipError_t upload(T** dst, const std::vector<T>& src) {
@@ -93,6 +94,7 @@ LeopardResult ensure_device(int dev, DeviceTables** out) {
         HIP_OK(upload(&d.sktab8, g_h_sktab8), "upload FF8 skew tables");
         HIP_OK(upload(&d.sktab16, g_h_sktab16), "upload FF16 skew tables");
         HIP_OK(upload(&d.fused8, g_h_fused8), "upload FF8 fused tables");
+        HIP_OK(upload(&d.fused16, g_h_fused16), "upload FF16 fused indices");
         HIP_OK(upload(&d.walsh8, g_h_walsh8), "upload FF8 LogWalsh");
         HIP_OK(upload(&d.walsh16, g_h_walsh16), "upload FF16 LogWalsh");
         HIP_OK(hipMalloc(reinterpret_cast<void**>(&d.zeros), 4096), "zero page");
@@ -343,6 +345,7 @@ LeopardResult encode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
     a.sktab = ff16 ? c.t->sktab16 : c.t->sktab8;
     a.tabs = ff16 ? c.t->tab16 : c.t->tab8;
     a.zeros = c.t->zeros;
+    a.fused = c.t->fused16 + fused16_base(Tm);
     a.K = K;
     a.R = R;
     a.Tm = Tm;
@@ -973,6 +976,7 @@ LEO_EXPORT int leo_init_(int version) {
     build_skew_tables(f8, g_h_tab8, kTab8Dwords, kSkewFlagDw8, g_h_sktab8);
     build_skew_tables(f16, g_h_tab16, kTab16Dwords, kSkewFlagDw16, g_h_sktab16);
     build_fused_top_tables8(f8, g_h_tab8, g_h_fused8);
+    build_fused_top_logs16(f16, g_h_fused16);
     g_h_walsh8.assign(f8.log_walsh.begin(), f8.log_walsh.end());
     g_h_walsh16.assign(f16.log_walsh.begin(), f16.log_walsh.end());
     g_dev.assign(count, DeviceTables{});

@@ -25,6 +25,7 @@ struct EncArgs {
     const uint32_t* sktab;  // butterfly tables indexed by skew position (gf_tables.h)
     const uint32_t* tabs;   // multiply tables by log value; entry kModulus+1 is all zero
     const uint8_t* zeros;   // >= 256 zero bytes
+    const uint32_t* fused;  // FF16: fused top-layer table index per chunk of this m (gf_tables.h)
     unsigned K, R, Tm, nchunks;
     uint64_t nunits;  // column units in this launch
 };

@@ -94,14 +94,16 @@ __global__ void __launch_bounds__(64 << wave_bits(T), 4) k_enc_fused(EncArgs a) 
     __syncthreads();
     TL::zero(acc);
     for (unsigned c = 0;;) {
+        // IFFT without its top layer, then the fused top (IFFT top + FFT top, as rs_ff8.hip)
         win.stage(a.sktab, int(m - 1 + c * m));
-        TL::ifft(x, w, lane, lds, ps, win, BelowLive{a.K - c * m});
+        TL::template ifft<true>(x, w, lane, lds, ps, win, BelowLive{a.K - c * m});
+        TL::fused_top(x, F::tab(a.tabs, cload(a.fused + c)));
         TL::xor_into(acc, x);
         if (++c >= a.nchunks) break;
         load_chunk(c);
     }
     win.stage(a.sktab, -1);
-    TL::fft(acc, w, lane, lds, ps, win, BelowLive{a.R});
+    TL::template fft<true>(acc, w, lane, lds, ps, win, BelowLive{a.R});
     TL::pin(acc);
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) {
@@ -163,12 +165,13 @@ __global__ void __launch_bounds__(64 << wave_bits(T), 4) k_enc_hi(EncArgs a) {
             load_or_zero<F>(x[r], a.slab_in, base + (tp << kLoBits) < a.K, base + ps.global(tp), a.zeros, ql);
         }
         win.stage(a.sktab, int(m - 1 + base));
-        TL::ifft(x, w, lane, lds, ps, win, BelowLive{a.K - base});
+        TL::template ifft<true>(x, w, lane, lds, ps, win, BelowLive{a.K - base});
+        TL::fused_top(x, F::tab(a.tabs, cload(a.fused + c)));  // top of the m-transform: this pass's top bit
         if (c == 0) TL::copy(acc, x);
         else TL::xor_into(acc, x);
     }
     win.stage(a.sktab, -1);
-    TL::fft(acc, w, lane, lds, ps, win, BelowLive{a.R});
+    TL::template fft<true>(acc, w, lane, lds, ps, win, BelowLive{a.R});
     if (!live) return;
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) {

@@ -118,8 +118,11 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         dist.init_process_group("gloo")  # control plane only (barrier, max-time); no data-path collective
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+    # one process per GPU; more ranks than GPUs (a functional rehearsal on a
+    # smaller box) share devices round-robin
+    gpu = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(gpu)
+    device = torch.device("cuda", gpu)
 
     import leopard_amd as leo
     from leopard_amd.sharding import max_over_ranks

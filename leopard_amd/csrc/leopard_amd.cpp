@@ -352,7 +352,12 @@ LeopardResult encode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
     a.nchunks = nchunks;
     const unsigned unit_bytes = ff16 ? 8 : 4;
 
-    const bool multipass = ff16 && Tm > kLoBits;
+    // Multi-pass for m > 2^kLoBits; also for m = 2^kLoBits with several chunks
+    // on narrow columns, where the single-tile kernel's one workgroup per
+    // 512-byte strip leaves CUs idle: pass 1 runs the chunk IFFTs in parallel
+    // workgroups and pass 3 combines them (no high pass).
+    const bool chunk_parallel = ff16 && Tm == kLoBits && nchunks > 1 && bytes / 8 < 1024 * 64;
+    const bool multipass = (ff16 && Tm > kLoBits) || chunk_parallel;
     uint64_t slice = bytes, slab_bytes = 0;
     if (multipass) {
         const uint64_t slab_pieces = uint64_t(nchunks) * m + m;
@@ -380,10 +385,14 @@ LeopardResult encode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
         b.slab_out = PieceMap{nullptr, U, slice, 0};
         b.nunits = len / unit_bytes;
         HIP_OK(launch_encode_lo(b, c.s), "encode pass 1");
-        b.slab_in = PieceMap{nullptr, U, slice, 0};
-        b.slab_out = PieceMap{nullptr, V, slice, 0};
-        HIP_OK(launch_encode_hi(b, c.s), "encode pass 2");
-        b.slab_in = PieceMap{nullptr, V, slice, 0};
+        if (!chunk_parallel) {
+            b.slab_in = PieceMap{nullptr, U, slice, 0};
+            b.slab_out = PieceMap{nullptr, V, slice, 0};
+            HIP_OK(launch_encode_hi(b, c.s), "encode pass 2");
+            b.slab_in = PieceMap{nullptr, V, slice, 0};
+        } else {
+            b.slab_in = PieceMap{nullptr, U, slice, 0};
+        }
         HIP_OK(launch_encode_fin(b, c.s), "encode pass 3");
     }
     return Leopard_Success;

@@ -180,7 +180,8 @@ __global__ void __launch_bounds__(64 << wave_bits(T), 4) k_enc_hi(EncArgs a) {
     }
 }
 
-// pass 3: FFT over the low bits, keep outputs g < R
+// pass 3: FFT over the low bits, keep outputs g < R.  When m = 2^kLoBits (no
+// high pass) the chunk IFFTs of pass 1 are combined here: x = XOR_c U[c*m + g].
 template <class F>
 __global__ void __launch_bounds__(64 << wave_bits(kLoBits), 4) k_enc_fin(EncArgs a) {
     constexpr int T = kLoBits;
@@ -195,6 +196,14 @@ __global__ void __launch_bounds__(64 << wave_bits(kLoBits), 4) k_enc_fin(EncArgs
     typename TL::Reg x;
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) load_units<F, C>(x[r], a.slab_in.ptr(ps.global(TL::piece(TL::kLast, r, w))), ql);
+    if (a.Tm == unsigned(kLoBits))
+        for (unsigned c = 1; c < a.nchunks; ++c) {
+            typename TL::Reg y;
+#pragma unroll
+            for (int r = 0; r < TL::NR; ++r)
+                load_units<F, C>(y[r], a.slab_in.ptr((c << T) + ps.global(TL::piece(TL::kLast, r, w))), ql);
+            TL::xor_into(x, y);
+        }
     win.stage(a.sktab, -1);
     TL::fft(x, w, lane, lds, ps, win, BelowLive{a.R});
     if (!live) return;

@@ -399,7 +399,10 @@ LDEV unsigned skew_index(unsigned i, unsigned l) { return ((i >> l) | 1u) << l; 
 // Layouts k = 0 .. NL-1 step upward through the bits (the last one holds the
 // top R bits); a butterfly layer on tile bit l runs in a layout holding bit l
 // in registers, and an LDS transpose moves the tile between adjacent layouts.
-template <class F, int T, int R, int C>
+// LW: lanes per tile column strip (64 = a wave per column strip; 32 or 16 when
+// the lane groups of a wave hold different pieces: "w" is then the virtual wave
+// index (wave and lane group) and "lane" the lane inside its group).
+template <class F, int T, int R, int C, int LW = 64>
 struct Tile {
     static_assert(R >= 1 && R <= T, "register bits");
     static constexpr int NR = 1 << R;         // pieces per lane
@@ -568,14 +571,14 @@ struct Tile {
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
-            uint32_t* p = lds + (size_t(piece(FROM, r, w)) * 64 + lane) * U;
+            uint32_t* p = lds + (size_t(piece(FROM, r, w)) * LW + lane) * U;
 #pragma unroll
             for (int k = 0; k < U; ++k) p[k] = x[r][k];
         }
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
-            const uint32_t* p = lds + (size_t(piece(TO, r, w)) * 64 + lane) * U;
+            const uint32_t* p = lds + (size_t(piece(TO, r, w)) * LW + lane) * U;
 #pragma unroll
             for (int k = 0; k < U; ++k) x[r][k] = p[k];
         }
@@ -592,7 +595,7 @@ struct Tile {
     //    issued: scalar loads return out of order, so a wait on one is a wait on
     //    every outstanding LDS and scalar read (lgkmcnt(0)).
     //  * Exchanges go through an LdsRing (one or two areas).
-    static constexpr size_t kAreaDwords = (size_t(1) << T) * 64 * U;
+    static constexpr size_t kAreaDwords = (size_t(1) << T) * LW * U;
     static constexpr int kMaxGroups = NR / 2 > 0 ? NR / 2 : 1;
     struct Look {
         typename F::Tab t[kMaxGroups];
@@ -680,14 +683,14 @@ struct Tile {
         if constexpr (Ring::kPreBarrier) __syncthreads();
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
-            uint32_t* p = area + (size_t(piece(FROM, r, w)) * 64 + lane) * U;
+            uint32_t* p = area + (size_t(piece(FROM, r, w)) * LW + lane) * U;
 #pragma unroll
             for (int k = 0; k < U; ++k) p[k] = x[r][k];
         }
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
-            const uint32_t* p = area + (size_t(piece(TO, r, w)) * 64 + lane) * U;
+            const uint32_t* p = area + (size_t(piece(TO, r, w)) * LW + lane) * U;
 #pragma unroll
             for (int k = 0; k < U; ++k) x[r][k] = p[k];
         }
@@ -743,7 +746,7 @@ struct Tile {
             if constexpr (Ring::kPreBarrier) __syncthreads();
 #pragma unroll
             for (int r = 0; r < NR; ++r) {
-                uint32_t* p = area + (size_t(piece(kLast, r, w)) * 64 + lane) * U;
+                uint32_t* p = area + (size_t(piece(kLast, r, w)) * LW + lane) * U;
 #pragma unroll
                 for (int k = 0; k < U; ++k) p[k] = v[r][k];
             }
@@ -762,7 +765,7 @@ struct Tile {
                 const unsigned w2 = w | (1u << b);
 #pragma unroll
                 for (int r = 0; r < NR; ++r) {
-                    const uint32_t* p = area + (size_t(piece(kLast, r, w2)) * 64 + lane) * U;
+                    const uint32_t* p = area + (size_t(piece(kLast, r, w2)) * LW + lane) * U;
 #pragma unroll
                     for (int k = 0; k < U; ++k) v[r][k] ^= p[k];
                 }
@@ -816,7 +819,7 @@ struct Tile {
             if (pre_barrier) __syncthreads();
 #pragma unroll
             for (int r = 0; r < NR; ++r) {
-                uint32_t* p = area + (size_t(piece(kLast, r, w)) * 64 + lane) * U;
+                uint32_t* p = area + (size_t(piece(kLast, r, w)) * LW + lane) * U;
 #pragma unroll
                 for (int k = 0; k < U; ++k) p[k] = v[r][k];
             }
@@ -840,7 +843,7 @@ struct Tile {
                 const unsigned w2 = w | (1u << b);
 #pragma unroll
                 for (int r = 0; r < NR; ++r) {
-                    const uint32_t* p = area + (size_t(piece(kLast, r, w2)) * 64 + lane) * U;
+                    const uint32_t* p = area + (size_t(piece(kLast, r, w2)) * LW + lane) * U;
 #pragma unroll
                     for (int k = 0; k < U; ++k) v[r][k] ^= p[k];
                 }
@@ -857,7 +860,7 @@ struct Tile {
             __syncthreads();
 #pragma unroll
             for (int r = 0; r < NR; ++r) {
-                uint32_t* p = lds + (size_t(piece(kLast, r, w)) * 64 + lane) * U;
+                uint32_t* p = lds + (size_t(piece(kLast, r, w)) * LW + lane) * U;
 #pragma unroll
                 for (int k = 0; k < U; ++k) p[k] = v[r][k];
             }
@@ -876,7 +879,7 @@ struct Tile {
                 const unsigned w2 = w | (1u << b);
 #pragma unroll
                 for (int r = 0; r < NR; ++r) {
-                    const uint32_t* p = lds + (size_t(piece(kLast, r, w2)) * 64 + lane) * U;
+                    const uint32_t* p = lds + (size_t(piece(kLast, r, w2)) * LW + lane) * U;
 #pragma unroll
                     for (int k = 0; k < U; ++k) v[r][k] ^= p[k];
                 }
@@ -902,7 +905,7 @@ struct Tile {
             __syncthreads();
 #pragma unroll
             for (int r = 0; r < NR; ++r) {
-                uint32_t* p = lds + (size_t(piece(kLast, r, w)) * 64 + lane) * U;
+                uint32_t* p = lds + (size_t(piece(kLast, r, w)) * LW + lane) * U;
 #pragma unroll
                 for (int k = 0; k < U; ++k) p[k] = v[r][k];
             }
@@ -912,7 +915,7 @@ struct Tile {
                 const unsigned w2 = w | (1u << b);
 #pragma unroll
                 for (int r = 0; r < NR; ++r) {
-                    const uint32_t* p = lds + (size_t(piece(kLast, r, w2)) * 64 + lane) * U;
+                    const uint32_t* p = lds + (size_t(piece(kLast, r, w2)) * LW + lane) * U;
 #pragma unroll
                     for (int k = 0; k < U; ++k) d[r][k] ^= p[k];
                 }

@@ -74,6 +74,17 @@ constexpr bool pipe8(int NA) { return kPipe8 && NA == 2; }
 constexpr int areas8(int NA) { return pipe8(NA) ? 2 : 1; }
 
 constexpr uint32_t kOneWgPerCuUnits = 256 * 64;  // 256 CUs x one 64-dword strip
+// Encoder lane groups (k_ff8_enc<..., G>): G = 1, 2 split a wave into 2^G
+// column strips of different pieces, so a 64 KiB call runs 2^G workgroups per
+// CU.  Bit-exact (tests/test_gpu_parity.py::test_encoder_lane_group_forms) but
+// measured slower on MI355X, 128+128 x 64 KiB encode: G = 0 10.4 us, G = 1
+// 11.5, G = 2 11.9 (per-workgroup table staging and per-lane-group table reads
+// outweigh the phase overlap; profiles/r01_v7/lane_groups_ab.txt), so the
+// default stays 0 and LEO_AMD_FF8_G selects the others for experiments.
+#ifndef LAMD_FF8_ENC_G
+#define LAMD_FF8_ENC_G 0
+#endif
+constexpr int kDefaultEncG = LAMD_FF8_ENC_G;
 
 // Piece pointers of the NR pieces a lane holds, fetched as one batch of scalar
 // loads: otherwise the compiler sinks each load into the branch that uses it,
@@ -99,6 +110,17 @@ LDEV Cols strip_cols(uint32_t nunits, unsigned lane) {
     const uint32_t left = nunits - first;
     return Cols{uint64_t(first) * 4, (lane < left ? lane : left - 1) * 4, lane < left};
 }
+// Strips of LW < 64 dwords (lane groups of a wave hold different pieces): the
+// strip index is XCD-major, so the neighbouring strips that share a 128-byte
+// line run on one XCD (workgroups are dealt round-robin over the 8 XCDs).
+template <int LW>
+LDEV Cols strip_cols_lw(uint32_t nunits, unsigned lane) {
+    const uint32_t nblk = gridDim.x, b = blockIdx.x;
+    const uint32_t s = (nblk & 7u) == 0 ? (b & 7u) * (nblk >> 3) + (b >> 3) : b;
+    const uint32_t first = s * uint32_t(LW);
+    const uint32_t left = nunits - first;
+    return Cols{uint64_t(first) * 4, (lane < left ? lane : left - 1) * 4, lane < left};
+}
 // piece pointer (kernel argument, wave-uniform) + strip base stay scalar: the
 // access is global_load/store with an SGPR base and the lane's VGPR offset.
 LDEV uint32_t gload(uint64_t piece, const Cols& c) {
@@ -110,30 +132,77 @@ LDEV void gstore(uint64_t piece, const Cols& c, uint32_t v) {
 
 // --------------------------------------------------------------- encode -----
 
-template <int T, int RB, bool kMulti, int NA>
-__global__ void __launch_bounds__(threads_for(T, RB), 4) k_ff8_enc(Ff8EncArgs a) {
+// A pruning predicate made wave-uniform: live if any lane's block is live (lane
+// groups hold different pieces).  Running the butterflies of a dead block is
+// harmless: an IFFT block without input stays zero, an FFT block without a
+// needed output feeds no needed output.
+template <class P>
+struct AnyLane {
+    P p;
+    LDEV bool operator()(unsigned pos, unsigned level) const {
+        return __builtin_amdgcn_ballot_w64(p(pos, level)) != 0;
+    }
+};
+template <int G, class P>
+LDEV auto lane_pred(const P& p) {
+    if constexpr (G == 0) return p;
+    else return AnyLane<P>{p};
+}
+
+template <int T, int RB, bool kMulti, int NA, int G>
+__global__ void __launch_bounds__(threads_for(T, RB) >> G, 4) k_ff8_enc(Ff8EncArgs a) {
     if constexpr ((LAMD_ABLATE & 16) != 0) return;
-    using TL = Tile<FF8, T, RB, 1>;
+    // G lane-group bits: the wave's 64 lanes hold 2^G column strips of LW lanes
+    // for different pieces (virtual wave w = lane group above the real wave), so
+    // a workgroup spans LW dwords of every piece and a 64 KiB call fills each CU
+    // with 2^G independent workgroups whose load / butterfly / store phases overlap.
+    constexpr int LW = 64 >> G;
+    using TL = Tile<FF8, T, RB, 1, LW>;
     constexpr unsigned m = 1u << T;
-    constexpr size_t kTile = tile_dwords_for(T, RB);
+    constexpr size_t kTile = tile_dwords_for(T, RB) >> G;
+    constexpr unsigned kThreads = threads_for(T, RB) >> G;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const LdsTab8<256> tabs{lds + areas8(NA) * kTile};
     LdsRing<kTile, areas8(NA)> ring{lds};
     STAMP(0);
-    TabStage8<threads_for(T, RB), 256> stage;
+    TabStage8<kThreads, 256> stage;
     stage.load(a.sktab);  // issued ahead of the piece loads
-    const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const Cols cl = strip_cols(a.nunits, lane);
+    const unsigned wave = uniform(threadIdx.x >> 6);
+    const unsigned lane = threadIdx.x & (LW - 1);
+    const unsigned w = G == 0 ? wave : (((threadIdx.x & 63u) >> (6 - G)) << (T - RB - G)) | wave;
+    const Cols cl = G == 0 ? strip_cols(a.nunits, lane) : strip_cols_lw<LW>(a.nunits, lane);
     const PieceSpace ps{0, 0, 0};
     typename TL::Reg x;
+    auto ptrs = [&](uint64_t (&pp)[TL::NR], auto idx) {
+        if constexpr (G == 0) fetch_ptrs(pp, a.ptr, idx);
+        else {
+#pragma unroll
+            for (int r = 0; r < TL::NR; ++r) pp[r] = a.ptr[idx(r)];  // per lane group
+        }
+    };
     auto load_chunk = [&](unsigned c) {
         const unsigned base = c * m;  // base + tp < nchunks * m <= K + m - 1 < 256
         uint64_t pp[TL::NR];
-        fetch_ptrs(pp, a.ptr, [&](int r) { return base + TL::piece(0, r, w); });
+        if constexpr (G == 0) {
+            ptrs(pp, [&](int r) { return base + TL::piece(0, r, w); });
 #pragma unroll
-        for (int r = 0; r < TL::NR; ++r) {
-            const unsigned i = base + TL::piece(0, r, w);
-            x[r][0] = i < a.K ? gload(pp[r], cl) : 0u;  // past K: zero padding (LeopardFF8.cpp:1631-1634)
+            for (int r = 0; r < TL::NR; ++r) {
+                const unsigned i = base + TL::piece(0, r, w);
+                x[r][0] = i < a.K ? gload(pp[r], cl) : 0u;  // past K: zero padding (LeopardFF8.cpp:1631-1634)
+            }
+        } else {
+            // per-lane pieces: branch-free, padding lanes re-read piece K - 1 and drop it
+            // (the exec-masked form of the conditional load in the chunk loop gave
+            // wrong results for a partial last chunk, e.g. 40 + 20 pieces)
+            ptrs(pp, [&](int r) {
+                const unsigned i = base + TL::piece(0, r, w);
+                return i < a.K ? i : a.K - 1;
+            });
+            uint32_t v[TL::NR];
+#pragma unroll
+            for (int r = 0; r < TL::NR; ++r) v[r] = gload(pp[r], cl);
+#pragma unroll
+            for (int r = 0; r < TL::NR; ++r) x[r][0] = base + TL::piece(0, r, w) < a.K ? v[r] : 0u;
         }
     };
     // IFFT / FFT of one stage: pipelined (lookahead tables, ring of two LDS areas) or plain
@@ -153,17 +222,17 @@ __global__ void __launch_bounds__(threads_for(T, RB), 4) k_ff8_enc(Ff8EncArgs a)
     LdsSkew8 win{tabs};
     if constexpr (!kMulti) {
         win.stage(nullptr, int(m - 1));
-        ifft(win, BelowLive{a.K});
+        ifft(win, lane_pred<G>(BelowLive{a.K}));
         STAMP(3);
         TL::fused_top(x, FF8::tab_at(a.fused));
         win.stage(nullptr, -1);
-        fft(win, BelowLive{a.R});
+        fft(win, lane_pred<G>(BelowLive{a.R}));
         STAMP(4);
     } else {
         typename TL::Reg acc;
         for (unsigned c = 0;;) {
             win.stage(nullptr, int(m - 1 + c * m));
-            ifft(win, BelowLive{a.K - c * m});
+            ifft(win, lane_pred<G>(BelowLive{a.K - c * m}));
             TL::fused_top(x, FF8::tab_at(a.fused + c * FF8::kTabDw));
             if (c == 0) TL::copy(acc, x);
             else TL::xor_into(acc, x);
@@ -172,11 +241,11 @@ __global__ void __launch_bounds__(threads_for(T, RB), 4) k_ff8_enc(Ff8EncArgs a)
         }
         TL::copy(x, acc);
         win.stage(nullptr, -1);
-        fft(win, BelowLive{a.R});
+        fft(win, lane_pred<G>(BelowLive{a.R}));
     }
     TL::pin(x);
     uint64_t pp[TL::NR];
-    fetch_ptrs(pp, a.ptr, [&](int r) { return a.K + TL::piece(0, r, w); });  // K + tp < K + m <= 256
+    ptrs(pp, [&](int r) { return a.K + TL::piece(0, r, w); });  // K + tp < K + m <= 256
     if (!cl.live) return;
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) {
@@ -283,18 +352,18 @@ struct Once {
     }
 };
 template <class Tag, class KernelFn, class Args>
-hipError_t launch8(KernelFn* fn, unsigned threads, const Args& a, size_t lds_dwords, hipStream_t s) {
+hipError_t launch8(KernelFn* fn, unsigned threads, const Args& a, size_t lds_dwords, hipStream_t s, unsigned lw = 64) {
     const size_t lds = lds_dwords * 4;
     if (lds > 65536) {
         const hipError_t e = Once<Tag>::set_lds(reinterpret_cast<const void*>(fn), lds);
         if (e != hipSuccess) return e;
     }
     void* params[] = {const_cast<Args*>(&a)};
-    const dim3 grid((a.nunits + 63) / 64);
+    const dim3 grid((a.nunits + lw - 1) / lw);
     return hipLaunchKernel(reinterpret_cast<const void*>(fn), grid, dim3(threads), params, lds, s);
 }
 
-template <int T, int RB, bool M, int NA>
+template <int T, int RB, bool M, int NA, int G>
 struct EncTag {};
 template <int T, int RB, int NA>
 struct DecTag {};
@@ -309,12 +378,34 @@ bool force_wide() {
     return v;
 }
 
+// Lane-group bits of the encoder launch (LEO_AMD_FF8_G overrides; read once):
+// pieces of at most 64 KiB run 64-byte strips (G = 2: four workgroups per CU
+// in a 64 KiB call), larger pieces the full-wave strips.
+int enc_lane_groups(uint32_t nunits) {
+    static const int v = [] {
+        const char* e = std::getenv("LEO_AMD_FF8_G");
+        return e && e[0] >= '0' && e[0] <= '2' ? e[0] - '0' : -1;
+    }();
+    if (v >= 0) return v;
+    return nunits <= 16384u ? kDefaultEncG : 0;
+}
+
+template <int T, int RB, int NA, int G>
+hipError_t enc_RBG(const Ff8EncArgs& a, hipStream_t s) {
+    constexpr size_t lds = areas8(NA) * (tile_dwords_for(T, RB) >> G) + LdsTab8<256>::kDwords;
+    constexpr unsigned threads = threads_for(T, RB) >> G;
+    if (a.nchunks > 1)
+        return launch8<EncTag<T, RB, true, NA, G>>(&k_ff8_enc<T, RB, true, NA, G>, threads, a, lds, s, 64u >> G);
+    return launch8<EncTag<T, RB, false, NA, G>>(&k_ff8_enc<T, RB, false, NA, G>, threads, a, lds, s, 64u >> G);
+}
 template <int T, int RB, int NA>
 hipError_t enc_RB(const Ff8EncArgs& a, hipStream_t s) {
-    constexpr size_t lds = areas8(NA) * tile_dwords_for(T, RB) + LdsTab8<256>::kDwords;
-    if (a.nchunks > 1)
-        return launch8<EncTag<T, RB, true, NA>>(&k_ff8_enc<T, RB, true, NA>, threads_for(T, RB), a, lds, s);
-    return launch8<EncTag<T, RB, false, NA>>(&k_ff8_enc<T, RB, false, NA>, threads_for(T, RB), a, lds, s);
+    if constexpr (NA == 1 && T - RB >= 2 && T > RB) {
+        const int g = enc_lane_groups(a.nunits);
+        if (g == 2) return enc_RBG<T, RB, NA, 2>(a, s);
+        if (g == 1) return enc_RBG<T, RB, NA, 1>(a, s);
+    }
+    return enc_RBG<T, RB, NA, 0>(a, s);
 }
 template <int T>
 hipError_t enc_T(const Ff8EncArgs& a, hipStream_t s) {

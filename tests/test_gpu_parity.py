@@ -340,3 +340,15 @@ def test_host_edge_paths(leo):
     assert leo.leo_decode(b, k, r, dwc, [d[i].ctypes.data for i in range(k)], [rec[i].ctypes.data for i in range(r)],
                           [dwork[i].ctypes.data for i in range(dwc)]) == 0
     assert np.array_equal(dwork[:k], d)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("groups", [1, 2])
+def test_encoder_lane_group_forms(groups):
+    """The lane-group encoder forms (LEO_AMD_FF8_G, read once per process) vs the oracle."""
+    import subprocess
+    import sys
+    env = dict(os.environ, LEO_AMD_FF8_G=str(groups))
+    tool = os.path.join(os.path.dirname(GOLDEN), "..", "tools", "probe_g.py")
+    res = subprocess.run([sys.executable, tool], env=env, capture_output=True, text=True, timeout=110)
+    assert res.returncode == 0, res.stdout + res.stderr

@@ -439,6 +439,15 @@ void error_locator8(const std::vector<uint32_t>& erased, uint32_t* el_bytes) {
     std::memcpy(el_bytes, last_el, sizeof(last_el));
 }
 
+// LEO_AMD_FF8_HALF=0 turns the half-position decoder off (A/B experiments); read once.
+bool ff8_half_decoder_enabled() {
+    static const bool v = [] {
+        const char* e = std::getenv("LEO_AMD_FF8_HALF");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
 LeopardResult decode_device8(Call& c, uint64_t bytes, uint64_t off, unsigned K, unsigned R, unsigned m, unsigned Tn,
                              const void* const* orig, const void* const* rec, void** work,
                              const std::vector<uint32_t>& erased) {
@@ -482,6 +491,15 @@ LeopardResult decode_device8(Call& c, uint64_t bytes, uint64_t off, unsigned K, 
     a.R = R;
     a.m = m;
     a.nunits = uint32_t(bytes / 4);
+    // No original survives and n = 2m: every received piece is in the low half of
+    // the positions, every output in the high half (k_ff8_dec_half, rs_ff8.hip).
+    bool any_orig = false;
+    for (unsigned i = 0; i < K; ++i) any_orig |= orig[i] != nullptr;
+    if (!any_orig && Tn >= 2 && 2 * m == (1u << Tn) && ff8_half_decoder_enabled()) {
+        a.fused = c.t->fused8 + size_t(Tn - 2) * 256 * kTab8Dwords;  // T = Tn - 1, chunk 0
+        HIP_OK(launch_ff8_decode_half(Tn - 1, a, c.s), "decode kernel");
+        return Leopard_Success;
+    }
     HIP_OK(launch_ff8_decode(Tn, a, c.s), "decode kernel");
     return Leopard_Success;
 }

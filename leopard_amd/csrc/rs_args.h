@@ -63,6 +63,7 @@ struct Ff8DecArgs {
     uint32_t el[kFf8Ptrs / 4];     // error locator logs (host computed), one byte per position
     const uint32_t* sktab;
     const uint32_t* tabs;          // multiply tables by log value; entry 256 is all zero
+    const uint32_t* fused;         // k_ff8_dec_half: fused top-layer table of this m (= encoder chunk 0's)
     unsigned K, R, m;
     uint32_t nunits;
 };
@@ -75,6 +76,7 @@ struct XorArgs {
 };
 
 // Launchers (rs_kernels.hip).  Return hipSuccess or the launch error.
+hipError_t launch_ff8_decode_half(unsigned Tm, const Ff8DecArgs& a, hipStream_t s);
 hipError_t launch_encode_fused16(unsigned T, const EncArgs& a, hipStream_t s);
 hipError_t launch_encode_lo(const EncArgs& a, hipStream_t s);
 hipError_t launch_encode_hi(const EncArgs& a, hipStream_t s);

@@ -340,6 +340,64 @@ __global__ void __launch_bounds__(threads_for(T, RB), 4) k_ff8_dec(Ff8DecArgs a)
     STAMP(6);
 }
 
+// Decode when every received piece sits in the low half of the positions (no
+// original survives; n = 2m, so recovery [0, R) is the low half and the lost
+// originals [m, m + K) the high half).  FFT (I + D) IFFT = F_low (swap_top +
+// D_low) I_low (Tile::derivative_swaptop), and F_low, D_low, I_low act inside
+// each half.  The high half of I_low(v) is zero, so after swap_top + D_low the
+// high half holds exactly the low half of I_low(v): the needed outputs are
+//   lost i = F_low,high( I_low,low( received * exp(el) ) )[i] * exp(-el[m + i])
+// -- an m-point IFFT on the low positions, an m-point FFT with the skews of the
+// high positions (the encoder's transform pair with the halves exchanged, so
+// the top layers fuse as in the encoder), no derivative, every wave busy (in k_ff8_dec the waves of the
+// empty high half idle through the scale and the low IFFT layers).
+template <int T, int RB>
+__global__ void __launch_bounds__(threads_for(T, RB), 4) k_ff8_dec_half(Ff8DecArgs a) {
+    if constexpr ((LAMD_ABLATE & 16) != 0) return;
+    using F = FF8;
+    using TL = Tile<F, T, RB, 1>;
+    constexpr unsigned m = 1u << T;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const LdsTab8<256> sk{lds + tile_dwords_for(T, RB)};
+    const LdsTab8<256> ltab{sk.base + LdsTab8<256>::kDwords};  // by log value
+    TabStage8<threads_for(T, RB), 256> sk_stage, log_stage;
+    sk_stage.load(a.sktab);
+    log_stage.load(a.tabs);
+    const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const Cols cl = strip_cols(a.nunits, lane);
+    const PieceSpace low{0, 0, 0}, high{0, 0, m};
+    const Pyr8Live present{a.present}, needed{a.needed};
+    auto lpos = [&](int r) { return TL::piece(0, r, w); };
+    auto hpos = [&](int r) { return m + TL::piece(0, r, w); };
+    typename TL::Reg v;
+    {
+        uint64_t pp[TL::NR];
+        fetch_ptrs(pp, a.ptr, lpos);
+#pragma unroll
+        for (int r = 0; r < TL::NR; ++r) v[r][0] = present(lpos(r), 0) ? gload(pp[r], cl) : 0u;
+    }
+    sk_stage.store(sk);
+    log_stage.store(ltab);
+    __syncthreads();
+    scale_batched<TL>(v, ltab, [&](int r) { return el_at(a, lpos(r)); }, [&](int r) { return present(lpos(r), 0); });
+    LdsSkew8 win{sk};
+    win.stage(nullptr, -1);  // decoder skew base (LeopardFF8.cpp:1880, 1903)
+    // both top layers (single skews m/2 - 1 and m + m/2 - 1) as one butterfly
+    // with their sum, the encoder's chunk-0 fused table (Tile::fused_top)
+    TL::template ifft<true>(v, w, lane, lds, low, win, present);
+    TL::fused_top(v, FF8::tab_at(a.fused));
+    TL::template fft<true>(v, w, lane, lds, high, win, needed);
+    TL::pin(v);
+    uint64_t pp[TL::NR];
+    fetch_ptrs(pp, a.ptr, hpos);
+    auto is_needed = [&](int r) { return needed(hpos(r), 0); };
+    scale_batched<TL>(v, ltab, [&](int r) { return F::kModulus - el_at(a, hpos(r)); }, is_needed);
+    if (!cl.live) return;
+#pragma unroll
+    for (int r = 0; r < TL::NR; ++r)
+        if (is_needed(r)) gstore(pp[r], cl, v[r][0]);
+}
+
 // Opting a kernel into > 64 KiB of LDS is a per-function attribute, set once
 // per kernel (Once is a distinct type per kernel instantiation).
 template <class Tag>
@@ -367,6 +425,8 @@ template <int T, int RB, bool M, int NA, int G>
 struct EncTag {};
 template <int T, int RB, int NA>
 struct DecTag {};
+template <int T, int RB>
+struct DecHalfTag {};
 
 // Launch shape overrides for experiments (LEO_AMD_FF8_WIDE=1: the wide
 // register forms at every size); read once.
@@ -430,6 +490,13 @@ hipError_t dec_T(const Ff8DecArgs& a, hipStream_t s) {
     return dec_RB<T, reg_bits8(T), 1>(a, s);
 }
 
+template <int T>
+hipError_t dec_half_T(const Ff8DecArgs& a, hipStream_t s) {
+    constexpr int RB = reg_bits8(T);
+    constexpr size_t lds = tile_dwords_for(T, RB) + 2 * LdsTab8<256>::kDwords;
+    return launch8<DecHalfTag<T, RB>>(&k_ff8_dec_half<T, RB>, threads_for(T, RB), a, lds, s);
+}
+
 }  // namespace
 
 #ifdef LAMD_STAMPS
@@ -442,6 +509,14 @@ hipError_t launch_ff8_encode(unsigned T, const Ff8EncArgs& a, hipStream_t s) {
     hipError_t e = hipErrorInvalidValue;
     static_for<1, 8>([&](auto I) {
         if (T == unsigned(decltype(I)::value)) e = enc_T<decltype(I)::value>(a, s);
+    });
+    return e;
+}
+
+hipError_t launch_ff8_decode_half(unsigned Tm, const Ff8DecArgs& a, hipStream_t s) {
+    hipError_t e = hipErrorInvalidValue;
+    static_for<1, 8>([&](auto I) {
+        if (Tm == unsigned(decltype(I)::value)) e = dec_half_T<decltype(I)::value>(a, s);
     });
     return e;
 }

@@ -90,7 +90,9 @@ def test_encode_host_memory_matches_oracle(leo):
 DEC_CASES = [  # (K, R, B, originals lost)
     (2, 2, 64, 1), (3, 2, 64, 2), (7, 5, 128, 5), (16, 16, 64, 9), (100, 20, 64, 20), (128, 128, 128, 128),
     (128, 128, 64, 1), (130, 126, 64, 100), (200, 55, 64, 55), (64, 64, 64 * 33, 40),
-    (129, 127, 64, 127), (300, 37, 128, 30), (1000, 200, 64, 200), (600, 300, 64, 299), (5000, 3000, 64, 3000),
+    (129, 127, 64, 127), (300, 37, 128, 30),
+    # every original lost (K = R, the half-position decoder), R not a power of 2
+    (90, 90, 64 * 5, 90), (3, 3, 64, 3), (33, 33, 256, 33), (1000, 200, 64, 200), (600, 300, 64, 299), (5000, 3000, 64, 3000),
 ]
 
 

@@ -439,7 +439,8 @@ void error_locator8(const std::vector<uint32_t>& erased, uint32_t* el_bytes) {
     std::memcpy(el_bytes, last_el, sizeof(last_el));
 }
 
-// LEO_AMD_FF8_HALF=0 turns the half-position decoder off (A/B experiments); read once.
+// LEO_AMD_FF8_HALF=0 turns the half-position decoders (FF8 kernel, FF16 pass 2)
+// off (A/B experiments); read once.
 bool ff8_half_decoder_enabled() {
     static const bool v = [] {
         const char* e = std::getenv("LEO_AMD_FF8_HALF");
@@ -587,6 +588,15 @@ LeopardResult decode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
     a.present_pyr = reinterpret_cast<uint32_t*>(c.ws->dbuf + off_pyr);
     a.needed_pyr = a.present_pyr + kPyrWords;
     a.nlo = (m + K + (1u << kLoBits) - 1) >> kLoBits;
+    // No original survives and n = 2m: the received pieces fill only the low half
+    // (k_dec_hi_half); pass 1 then runs the recovery tiles only.
+    bool any_orig = false;
+    for (unsigned i = 0; i < K; ++i) any_orig |= orig[i] != nullptr;
+    const bool half = !any_orig && Tn >= kLoBits + 2 && 2 * m == n && ff8_half_decoder_enabled();
+    if (half) {
+        a.nlo = (R + (1u << kLoBits) - 1) >> kLoBits;
+        a.fused = c.t->fused16 + fused16_base(Tn - 1);
+    }
 
     uint8_t* A = c.ws->dbuf + off_slab;
     uint8_t* Uu = A + uint64_t(n) * slice;
@@ -601,7 +611,7 @@ LeopardResult decode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
         HIP_OK(launch_decode_lo(b, c.s), "decode pass 1");
         b.a_in = PieceMap{nullptr, Uu, slice, 0};
         b.a_out = PieceMap{nullptr, A, slice, 0};
-        HIP_OK(launch_decode_hi(b, c.s), "decode pass 2");
+        HIP_OK(half ? launch_decode_hi_half(b, c.s) : launch_decode_hi(b, c.s), "decode pass 2");
         b.a_in = PieceMap{nullptr, A, slice, 0};
         b.b_in = PieceMap{nullptr, Uu, slice, 0};
         HIP_OK(launch_decode_fin(b, c.s), "decode pass 3");

@@ -41,6 +41,7 @@ struct DecArgs {
     const uint32_t* needed_pyr;   // FF16: "any lost original" pyramid over positions
     const uint32_t* el;          // FF16: precomputed error locator logs
     const uint32_t* erased_dev;  // FF16: erasure bitmap over positions [0, n)
+    const uint32_t* fused;       // FF16 half-position pass 2: fused top-layer table index of this m
     unsigned K, R, m, Tn, nlo;   // nlo: number of non-zero low tiles
     uint64_t nunits;
 };
@@ -76,6 +77,7 @@ struct XorArgs {
 };
 
 // Launchers (rs_kernels.hip).  Return hipSuccess or the launch error.
+hipError_t launch_decode_hi_half(const DecArgs& a, hipStream_t s);
 hipError_t launch_ff8_decode_half(unsigned Tm, const Ff8DecArgs& a, hipStream_t s);
 hipError_t launch_encode_fused16(unsigned T, const EncArgs& a, hipStream_t s);
 hipError_t launch_encode_lo(const EncArgs& a, hipStream_t s);

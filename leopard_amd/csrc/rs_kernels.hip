@@ -332,6 +332,36 @@ __global__ void __launch_bounds__(64 << wave_bits(T), 4) k_dec_hi(DecArgs a) {
         for (int r = 0; r < TL::NR; ++r) store_units<F, C>(a.a_out.ptr(ps.global(TL::piece(0, r, w))), q0, v[r]);
 }
 
+// pass 2 when every received piece is in the low half (K = R, every original
+// lost; see k_ff8_dec_half in rs_ff8.hip): the high IFFT layers of the low
+// half, the fused top layer of the m-transform (encoder chunk 0's table) and the
+// high FFT layers with the skews of the high half; A is written at the high
+// positions only and pass 3 adds D_lo(U) = 0 there (U has no high tiles).
+template <class F, int T>
+__global__ void __launch_bounds__(64 << wave_bits(T), 4) k_dec_hi_half(DecArgs a) {
+    using TL = Tile<F, T, reg_bits(T), C>;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    GlobalWindow<F> win;
+    const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const uint64_t q0 = lane_units(lane);
+    const bool live = q0 < a.nunits;
+    const uint64_t ql = live ? q0 : a.nunits - C;
+    const PieceSpace low{blockIdx.y, kLoBits, 0}, high{blockIdx.y, kLoBits, a.m};
+    typename TL::Reg v;
+#pragma unroll
+    for (int r = 0; r < TL::NR; ++r) {
+        const unsigned tp = TL::piece(0, r, w);
+        load_or_zero<F>(v[r], a.a_in, tp < a.nlo, low.global(tp), a.zeros, ql);
+    }
+    win.stage(a.sktab, -1);
+    TL::template ifft<true>(v, w, lane, lds, low, win, Pyr16Live{a.present_pyr});
+    TL::fused_top(v, F::tab(a.tabs, cload(a.fused)));
+    TL::template fft<true>(v, w, lane, lds, high, win, Pyr16Live{a.needed_pyr});
+    if (live)
+#pragma unroll
+        for (int r = 0; r < TL::NR; ++r) store_units<F, C>(a.a_out.ptr(high.global(TL::piece(0, r, w))), q0, v[r]);
+}
+
 // pass 3: z = A + D_lo(U), FFT over the low bits, reveal lost originals (U of
 // a low tile without received data is zero and was never written)
 template <class F>
@@ -479,6 +509,14 @@ struct DecHiFn {
     }
 };
 
+template <class F, int T>
+struct DecHiHalfFn {
+    static hipError_t run(const DecArgs& a, hipStream_t s) {
+        return launch(&k_dec_hi_half<F, T>, dim3(tiles_for(a.nunits), 1u << kLoBits), 64u << wave_bits(T),
+                      full_tile_lds<F, T>(), s, &a);
+    }
+};
+
 template <template <class, int> class Fn, class F, int TMIN, int TMAX, class A>
 hipError_t dispatch_T(unsigned T, const A& a, hipStream_t s) {
     hipError_t e = hipErrorInvalidValue;
@@ -512,6 +550,9 @@ hipError_t launch_decode_lo(const DecArgs& a, hipStream_t s) {
 }
 hipError_t launch_decode_hi(const DecArgs& a, hipStream_t s) {
     return dispatch_T<DecHiFn, FF16, 1, 8>(a.Tn - kLoBits, a, s);
+}
+hipError_t launch_decode_hi_half(const DecArgs& a, hipStream_t s) {
+    return dispatch_T<DecHiHalfFn, FF16, 1, 7>(a.Tn - 1 - kLoBits, a, s);
 }
 hipError_t launch_decode_fin(const DecArgs& a, hipStream_t s) {
     const unsigned n = 1u << a.Tn;

@@ -92,7 +92,9 @@ DEC_CASES = [  # (K, R, B, originals lost)
     (128, 128, 64, 1), (130, 126, 64, 100), (200, 55, 64, 55), (64, 64, 64 * 33, 40),
     (129, 127, 64, 127), (300, 37, 128, 30),
     # every original lost (K = R, the half-position decoder), R not a power of 2
-    (90, 90, 64 * 5, 90), (3, 3, 64, 3), (33, 33, 256, 33), (1000, 200, 64, 200), (600, 300, 64, 299), (5000, 3000, 64, 3000),
+    (90, 90, 64 * 5, 90), (3, 3, 64, 3), (33, 33, 256, 33),
+    (300, 300, 128, 300), (600, 600, 64, 600), (2000, 2000, 64, 2000),  # FF16 half-position pass 2
+    (1000, 200, 64, 200), (600, 300, 64, 299), (5000, 3000, 64, 3000),
 ]
 
 

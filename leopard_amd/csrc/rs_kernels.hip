@@ -381,15 +381,17 @@ __global__ void __launch_bounds__(64 << wave_bits(kLoBits), 4) k_dec_fin(DecArgs
     const uint64_t ql = live ? q0 : a.nunits - C;
     const PieceSpace ps{0, 0, blockIdx.y << T};
     const State16 st{a.erased_dev, a.el, a.tabs};
-    typename TL::Reg z, v;
+    typename TL::Reg z;
 #pragma unroll
-    for (int r = 0; r < TL::NR; ++r) {
-        const unsigned g = ps.global(TL::piece(TL::kLast, r, w));
-        load_units<F, C>(z[r], a.a_in.ptr(g), ql);
-        load_or_zero<F>(v[r], a.b_in, blockIdx.y < a.nlo, g, a.zeros, ql);
-    }
+    for (int r = 0; r < TL::NR; ++r) load_units<F, C>(z[r], a.a_in.ptr(ps.global(TL::piece(TL::kLast, r, w))), ql);
     win.stage(a.sktab, -1);
-    TL::derivative_add(z, v, w, lane, lds);
+    // U of a tile past the received ones is zero, and so is D_lo(U) (workgroup-uniform)
+    if (blockIdx.y < a.nlo) {
+        typename TL::Reg v;
+#pragma unroll
+        for (int r = 0; r < TL::NR; ++r) load_units<F, C>(v[r], a.b_in.ptr(ps.global(TL::piece(TL::kLast, r, w))), ql);
+        TL::derivative_add(z, v, w, lane, lds);
+    }
     TL::fft(z, w, lane, lds, ps, win, Pyr16Live{a.needed_pyr});
     if (!live) return;
 #pragma unroll

@@ -105,10 +105,14 @@ LeopardResult ensure_device(int dev, DeviceTables** out) {
     return Leopard_Success;
 }
 
-// Per-thread, per-device scratch: device arena (grow-only) plus a pinned host
-// staging area for pointer tables / bitmaps.
+// Scratch of one (thread, device, stream): device arena (grow-only) plus a
+// pinned host staging area for pointer tables / bitmaps.  Keyed by stream as
+// well as by device: the kernels of a call read the arena after the call
+// returns (async mode), and only calls on the same stream are ordered after
+// them, so two streams must never share one arena.
 struct Workspace {
     int dev = -1;
+    hipStream_t stream = nullptr;
     uint8_t* dbuf = nullptr;
     size_t dsize = 0;
     uint8_t* hstage = nullptr;
@@ -123,6 +127,14 @@ struct Workspace {
     hipStream_t pipe_stream[2] = {nullptr, nullptr};
     hipEvent_t in_done[2] = {nullptr, nullptr};
     hipEvent_t out_done[2] = {nullptr, nullptr};
+    // GF(2^16) decoder state kept on the device across calls (its own
+    // allocation, so the arena above can be reused by every other call):
+    // erasure bitmap, the two occupancy pyramids, the error locator and its
+    // FWHT scratch.  dec16_key holds the (K, R, bitmap) the state was built
+    // for: a repeated erasure pattern re-uploads nothing and skips the
+    // error-locator launches.
+    uint8_t* dec16 = nullptr;
+    std::vector<uint32_t> dec16_key;
 
     ~Workspace() {
         // Process teardown: the runtime may already be gone; leak rather than crash.
@@ -177,13 +189,13 @@ struct Workspace {
 };
 thread_local std::vector<std::unique_ptr<Workspace>> tws;
 
-Workspace& workspace(int dev) {
-    if (int(tws.size()) <= dev) tws.resize(dev + 1);
-    if (!tws[dev]) {
-        tws[dev] = std::make_unique<Workspace>();
-        tws[dev]->dev = dev;
-    }
-    return *tws[dev];
+Workspace& workspace(int dev, hipStream_t stream) {
+    for (auto& w : tws)
+        if (w->dev == dev && w->stream == stream) return *w;
+    tws.push_back(std::make_unique<Workspace>());
+    tws.back()->dev = dev;
+    tws.back()->stream = stream;
+    return *tws.back();
 }
 
 // ------------------------------------------------------------ call helpers --
@@ -271,6 +283,9 @@ struct MapBuilder {
     }
 };
 
+// Columns per GF(2^8) launch: its argument block counts dword columns in 32 bits.
+constexpr uint64_t kFf8MaxLaunchBytes = 1ull << 32;
+
 // Column range processed per pass sequence of the multi-pass FF16 kernels:
 // keep the intermediates (pieces x slice) around the 256 MiB Infinity Cache.
 uint64_t mall_budget() {
@@ -299,8 +314,8 @@ LeopardResult begin_call(int dev, Call& c) {
     LeopardResult r = ensure_device(dev, &c.t);
     if (r != Leopard_Success) return r;
     c.dev = dev;
-    c.ws = &workspace(dev);
     c.s = tls.stream;
+    c.ws = &workspace(dev, c.s);
     return Leopard_Success;
 }
 
@@ -325,15 +340,18 @@ LeopardResult encode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
     if (!ff16) {  // n <= 256: one fused kernel, launch data by value (rs_ff8.hip)
         Ff8EncArgs a;
         std::memset(&a, 0, sizeof(a));
-        for (unsigned i = 0; i < K; ++i) a.ptr[i] = uint64_t(reinterpret_cast<uintptr_t>(orig[i])) + off;
-        for (unsigned i = 0; i < R; ++i) a.ptr[K + i] = uint64_t(reinterpret_cast<uintptr_t>(work[i])) + off;
         a.sktab = c.t->sktab8;
         a.fused = c.t->fused8 + size_t(Tm - 1) * 256 * kTab8Dwords;
         a.K = K;
         a.R = R;
         a.nchunks = nchunks;
-        a.nunits = uint32_t(bytes / 4);
-        HIP_OK(launch_ff8_encode(Tm, a, c.s), "encode kernel");
+        // one launch per <= 4 GiB of columns (the kernel counts dword columns in 32 bits)
+        for (uint64_t pos = 0; pos < bytes; pos += kFf8MaxLaunchBytes) {
+            for (unsigned i = 0; i < K; ++i) a.ptr[i] = uint64_t(reinterpret_cast<uintptr_t>(orig[i])) + off + pos;
+            for (unsigned i = 0; i < R; ++i) a.ptr[K + i] = uint64_t(reinterpret_cast<uintptr_t>(work[i])) + off + pos;
+            a.nunits = uint32_t(std::min(kFf8MaxLaunchBytes, bytes - pos) / 4);
+            HIP_OK(launch_ff8_encode(Tm, a, c.s), "encode kernel");
+        }
         return Leopard_Success;
     }
 
@@ -460,11 +478,13 @@ LeopardResult decode_device8(Call& c, uint64_t bytes, uint64_t off, unsigned K, 
             pyr[pyr8_offset(L) + (j >> 5)] |= 1u << (j & 31);
         }
     };
-    auto addr = [&](const void* p) { return uint64_t(reinterpret_cast<uintptr_t>(p)) + off; };
-    for (unsigned i = 0; i < R; ++i)
-        if (rec[i]) a.ptr[i] = addr(rec[i]);
-    for (unsigned i = 0; i < K; ++i)
-        a.ptr[m + i] = addr(orig[i] ? orig[i] : work[i]);  // lost: its slot carries the output
+    auto set_ptrs = [&](uint64_t pos) {
+        auto addr = [&](const void* p) { return uint64_t(reinterpret_cast<uintptr_t>(p)) + off + pos; };
+        for (unsigned i = 0; i < R; ++i)
+            if (rec[i]) a.ptr[i] = addr(rec[i]);
+        for (unsigned i = 0; i < K; ++i)
+            a.ptr[m + i] = addr(orig[i] ? orig[i] : work[i]);  // lost: its slot carries the output
+    };
     // The pyramids depend only on (K, R, erasure pattern); the last pattern is
     // cached per thread (repeated patterns are the common case).
     struct PyrCache {
@@ -491,17 +511,17 @@ LeopardResult decode_device8(Call& c, uint64_t bytes, uint64_t off, unsigned K, 
     a.K = K;
     a.R = R;
     a.m = m;
-    a.nunits = uint32_t(bytes / 4);
     // No original survives and n = 2m: every received piece is in the low half of
     // the positions, every output in the high half (k_ff8_dec_half, rs_ff8.hip).
     bool any_orig = false;
     for (unsigned i = 0; i < K; ++i) any_orig |= orig[i] != nullptr;
-    if (!any_orig && Tn >= 2 && 2 * m == (1u << Tn) && ff8_half_decoder_enabled()) {
-        a.fused = c.t->fused8 + size_t(Tn - 2) * 256 * kTab8Dwords;  // T = Tn - 1, chunk 0
-        HIP_OK(launch_ff8_decode_half(Tn - 1, a, c.s), "decode kernel");
-        return Leopard_Success;
+    const bool half = !any_orig && Tn >= 2 && 2 * m == (1u << Tn) && ff8_half_decoder_enabled();
+    if (half) a.fused = c.t->fused8 + size_t(Tn - 2) * 256 * kTab8Dwords;  // T = Tn - 1, chunk 0
+    for (uint64_t pos = 0; pos < bytes; pos += kFf8MaxLaunchBytes) {  // see encode_device
+        set_ptrs(pos);
+        a.nunits = uint32_t(std::min(kFf8MaxLaunchBytes, bytes - pos) / 4);
+        HIP_OK(half ? launch_ff8_decode_half(Tn - 1, a, c.s) : launch_ff8_decode(Tn, a, c.s), "decode kernel");
     }
-    HIP_OK(launch_ff8_decode(Tn, a, c.s), "decode kernel");
     return Leopard_Success;
 }
 
@@ -539,53 +559,78 @@ LeopardResult decode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
     a.Tn = Tn;
 
     // FF16: erasure bitmap (full 65536 positions) + error locator on the device,
-    // plus occupancy pyramids for pruning (received data / lost originals).
+    // plus occupancy pyramids for pruning (received data / lost originals), in
+    // the workspace's persistent decoder state (rebuilt only when the erasure
+    // pattern changes).
     const size_t bitmap_words = 65536 / 32;
-    std::vector<uint32_t> pyr_present(kPyrWords, 0), pyr_needed(kPyrWords, 0);
-    {
-        auto mark = [](std::vector<uint32_t>& pyr, unsigned p) {
-            for (unsigned L = 0; L <= 16; ++L) {
-                const unsigned j = p >> L;
-                pyr[pyr_offset(L) + (j >> 5)] |= 1u << (j & 31);
-            }
-        };
-        for (unsigned i = 0; i < R; ++i)
-            if (rec[i]) mark(pyr_present, i);
-        for (unsigned i = 0; i < K; ++i) mark(orig[i] ? pyr_present : pyr_needed, m + i);
-    }
+    const size_t off_pyr = bitmap_words * 4;
+    const size_t pyr_bytes = (2 * kPyrWords * 4 + 255) / 256 * 256;
+    const size_t off_tmp = off_pyr + pyr_bytes;
+    const size_t off_el = off_tmp + 65536 * 4;
+    const size_t off_sl = off_el + 65536 * 4;
+    const size_t off_rl = off_sl + 65536 * 4;
+    const size_t dec16_bytes = off_rl + 65536 * 4;
+    Workspace& ws = *c.ws;
+    if (!ws.dec16) HIP_OK(hipMalloc(reinterpret_cast<void**>(&ws.dec16), dec16_bytes), "allocate decoder state");
+    std::vector<uint32_t> key(2 + bitmap_words, 0);
+    key[0] = K;
+    key[1] = R;
+    std::copy(erased.begin(), erased.end(), key.begin() + 2);
+    const bool rebuild = key != ws.dec16_key;
+
     const uint64_t slab_pieces = 2ull * n;  // U (pass 1 -> 2, 3) and A (pass 2 -> 3)
     const uint64_t slice = mall_slice(bytes, slab_pieces);
     const size_t table_bytes = (mb.bytes() + 255) / 256 * 256;
-    const size_t off_bitmap = table_bytes;
-    const size_t off_tmp = off_bitmap + bitmap_words * 4;
-    const size_t off_el = off_tmp + 65536 * 4;
-    const size_t off_pyr = off_el + 65536 * 4;
-    const size_t off_slab = off_pyr + 2 * kPyrWords * 4 + 256;
-    LeopardResult r = c.ws->reserve_device(off_slab + slab_pieces * slice);
+    const size_t off_slab = table_bytes;
+    LeopardResult r = ws.reserve_device(off_slab + slab_pieces * slice);
     if (r != Leopard_Success) return r;
-    // stage tables + bitmap together
-    std::vector<uint32_t> bitmap(bitmap_words, 0);
-    std::copy(erased.begin(), erased.end(), bitmap.begin());
-    // staged image mirrors the device layout from offset 0 up to the slabs
-    const size_t stage_bytes = off_slab;
-    r = c.ws->reserve_stage(stage_bytes);
-    if (r != Leopard_Success) return r;
-    if (!mb.staged.empty()) std::memcpy(c.ws->hstage, mb.staged.data(), mb.bytes());
-    std::memcpy(c.ws->hstage + off_bitmap, bitmap.data(), bitmap_words * 4);
-    std::memcpy(c.ws->hstage + off_pyr, pyr_present.data(), kPyrWords * 4);
-    std::memcpy(c.ws->hstage + off_pyr + kPyrWords * 4, pyr_needed.data(), kPyrWords * 4);
-    HIP_OK(hipMemcpyAsync(c.ws->dbuf, c.ws->hstage, stage_bytes, hipMemcpyHostToDevice, c.s), "upload decode state");
-    HIP_OK(hipEventRecord(c.ws->stage_done, c.s), "record staging");
-    c.ws->stage_pending = true;
-    for (auto& p : mb.pending) p.map->table = reinterpret_cast<uint64_t*>(c.ws->dbuf) + p.index;
+    // one staging image: piece tables (if any) then, on a new pattern, bitmap + pyramids
+    const size_t stage_bytes = table_bytes + (rebuild ? off_tmp : 0);
+    if (stage_bytes) {
+        r = ws.reserve_stage(stage_bytes);
+        if (r != Leopard_Success) return r;
+        if (!mb.staged.empty()) {
+            std::memcpy(ws.hstage, mb.staged.data(), mb.bytes());
+            HIP_OK(hipMemcpyAsync(ws.dbuf, ws.hstage, mb.bytes(), hipMemcpyHostToDevice, c.s), "upload piece tables");
+        }
+        if (rebuild) {
+            uint8_t* h = ws.hstage + table_bytes;
+            std::memset(h, 0, off_tmp);
+            std::memcpy(h, erased.data(), erased.size() * 4);
+            uint32_t* pp = reinterpret_cast<uint32_t*>(h + off_pyr);
+            uint32_t* pn = pp + kPyrWords;
+            auto mark = [](uint32_t* pyr, unsigned p) {
+                for (unsigned L = 0; L <= 16; ++L) {
+                    const unsigned j = p >> L;
+                    pyr[pyr_offset(L) + (j >> 5)] |= 1u << (j & 31);
+                }
+            };
+            for (unsigned i = 0; i < R; ++i)
+                if (rec[i]) mark(pp, i);
+            for (unsigned i = 0; i < K; ++i) mark(orig[i] ? pp : pn, m + i);
+            HIP_OK(hipMemcpyAsync(ws.dec16, h, off_tmp, hipMemcpyHostToDevice, c.s), "upload decode state");
+        }
+        HIP_OK(hipEventRecord(ws.stage_done, c.s), "record staging");
+        ws.stage_pending = true;
+    }
+    for (auto& p : mb.pending) p.map->table = reinterpret_cast<uint64_t*>(ws.dbuf) + p.index;
 
-    uint32_t* d_bitmap = reinterpret_cast<uint32_t*>(c.ws->dbuf + off_bitmap);
-    uint32_t* d_tmp = reinterpret_cast<uint32_t*>(c.ws->dbuf + off_tmp);
-    uint32_t* d_el = reinterpret_cast<uint32_t*>(c.ws->dbuf + off_el);
-    HIP_OK(launch_error_locator16(d_bitmap, c.t->walsh16, d_tmp, d_el, c.s), "error locator");
+    uint32_t* d_bitmap = reinterpret_cast<uint32_t*>(ws.dec16);
+    uint32_t* d_tmp = reinterpret_cast<uint32_t*>(ws.dec16 + off_tmp);
+    uint32_t* d_el = reinterpret_cast<uint32_t*>(ws.dec16 + off_el);
+    uint32_t* d_sl = reinterpret_cast<uint32_t*>(ws.dec16 + off_sl);
+    uint32_t* d_rl = reinterpret_cast<uint32_t*>(ws.dec16 + off_rl);
+    if (rebuild) {
+        ws.dec16_key.clear();  // stays invalid if the launch fails
+        HIP_OK(launch_error_locator16(d_bitmap, c.t->walsh16, d_tmp, d_el, d_sl, d_rl, m, K, R, c.s),
+               "error locator");
+        ws.dec16_key = std::move(key);
+    }
     a.el = d_el;
+    a.scale_logs = d_sl;
+    a.reveal_logs = d_rl;
     a.erased_dev = d_bitmap;
-    a.present_pyr = reinterpret_cast<uint32_t*>(c.ws->dbuf + off_pyr);
+    a.present_pyr = reinterpret_cast<uint32_t*>(ws.dec16 + off_pyr);
     a.needed_pyr = a.present_pyr + kPyrWords;
     a.nlo = (m + K + (1u << kLoBits) - 1) >> kLoBits;
     // No original survives and n = 2m: the received pieces fill only the low half
@@ -598,7 +643,7 @@ LeopardResult decode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
         a.fused = c.t->fused16 + fused16_base(Tn - 1);
     }
 
-    uint8_t* A = c.ws->dbuf + off_slab;
+    uint8_t* A = ws.dbuf + off_slab;
     uint8_t* Uu = A + uint64_t(n) * slice;
     for (uint64_t pos = 0; pos < bytes; pos += slice) {
         const uint64_t len = std::min(slice, bytes - pos);

@@ -42,6 +42,8 @@ struct DecArgs {
     const uint32_t* el;          // FF16: precomputed error locator logs
     const uint32_t* erased_dev;  // FF16: erasure bitmap over positions [0, n)
     const uint32_t* fused;       // FF16 half-position pass 2: fused top-layer table index of this m
+    const uint32_t* scale_logs;  // FF16: log value of the scale multiply per position (65536 = zero table)
+    const uint32_t* reveal_logs; // FF16: log value of the reveal multiply per position
     unsigned K, R, m, Tn, nlo;   // nlo: number of non-zero low tiles
     uint64_t nunits;
 };
@@ -87,6 +89,7 @@ hipError_t launch_decode_lo(const DecArgs& a, hipStream_t s);
 hipError_t launch_decode_hi(const DecArgs& a, hipStream_t s);
 hipError_t launch_decode_fin(const DecArgs& a, hipStream_t s);
 hipError_t launch_error_locator16(const uint32_t* erased, const uint32_t* walsh, uint32_t* tmp, uint32_t* el,
+                                  uint32_t* scale_logs, uint32_t* reveal_logs, unsigned m, unsigned K, unsigned R,
                                   hipStream_t s);
 hipError_t launch_xor_reduce(const XorArgs& a, hipStream_t s);
 hipError_t launch_ff8_encode(unsigned T, const Ff8EncArgs& a, hipStream_t s);

@@ -295,6 +295,76 @@ struct GlobalWindow {
     LDEV void stage(const uint32_t* sktab, int off) { sk = sktab + ptrdiff_t(off) * ptrdiff_t(F::kTabDw); }
 };
 
+// FF16 butterfly tables of one transform stage staged in LDS (Tabs16Stage):
+// slot j (1 <= j < 2^T) of a set holds the table of skew position
+// base + hi_fixed + (j << l0).  Those are exactly the positions a tile of
+// PieceSpace{lo_fixed, l0, hi_fixed} asks for on its layers: for a layer on
+// global bit l >= l0, skew_index(i, l) = hi_fixed + (j << l0) with
+// j = ((tile piece >> (l - l0)) | 1) << (l - l0).  A table is five
+// ds_read_b128 at a wave-uniform address into VGPRs, so v_perm takes both
+// table dwords from VGPRs (SGPR tables cost a v_mov per perm pair) and no
+// scalar-load round trip sits in front of every butterfly group.
+struct LdsWindow16 {
+    const uint32_t* set;
+    unsigned hi_fixed, l0;
+    LDEV FF16::Tab table(unsigned cidx) const { return FF16::tab_lds(set + ((cidx - hi_fixed) >> l0) * 20u); }
+    LDEV void stage(const uint32_t*, int) {}
+};
+constexpr size_t kTab16LdsDwords = 20;
+
+// Cooperative global -> LDS copy of one set of 2^T FF16 skew tables (see
+// LdsWindow16), split like TabStage8: load() issues the global loads (ahead of
+// the piece loads), store() writes LDS after the piece loads are in flight.
+template <int NT, int T>
+struct Tabs16Stage {
+    static constexpr unsigned kVec = ((1u << T) - 1) * 5;  // uint4 per set (slot 0 unused)
+    static constexpr unsigned PER = (kVec + NT - 1) / NT;
+    uint4 v[PER];
+    LDEV void load(const uint32_t* sktab, int base, unsigned hi_fixed, unsigned l0) {
+        static_for<0, int(PER)>([&](auto I) __attribute__((always_inline)) {
+            constexpr unsigned i = decltype(I)::value;
+            unsigned e = threadIdx.x + i * NT;
+            if constexpr ((i + 1) * NT > kVec) e = e < kVec ? e : kVec - 1;
+            const unsigned j = 1 + e / 5, k = e % 5;
+            const size_t entry = size_t(int64_t(base) + int64_t(hi_fixed + (j << l0)));
+            v[i] = reinterpret_cast<const uint4*>(sktab)[entry * 6 + k];  // 24-dword entries
+        });
+    }
+    LDEV void store(uint32_t* set) const {
+        static_for<0, int(PER)>([&](auto I) __attribute__((always_inline)) {
+            constexpr unsigned i = decltype(I)::value;
+            const unsigned e = threadIdx.x + i * NT;
+            if ((i + 1) * NT <= kVec || e < kVec) reinterpret_cast<uint4*>(set)[5 + e] = v[i];
+        });
+    }
+};
+
+// Cooperative copy of the FF16 multiply tables of N log values into LDS: slot
+// p = the table of log value logs[p] (tab16: 24 dwords per log value; 65536 =
+// the all-zero table).  The decoder's per-piece scale and reveal multiplies.
+template <int NT, unsigned N>
+struct LogTabs16Stage {
+    static constexpr unsigned kVec = N * 5;
+    static constexpr unsigned PER = (kVec + NT - 1) / NT;
+    uint4 v[PER];
+    LDEV void load(const uint32_t* tabs, const uint32_t* logs) {
+        static_for<0, int(PER)>([&](auto I) __attribute__((always_inline)) {
+            constexpr unsigned i = decltype(I)::value;
+            unsigned e = threadIdx.x + i * NT;
+            if constexpr ((i + 1) * NT > kVec) e = e < kVec ? e : kVec - 1;
+            const unsigned lm = logs[e / 5];
+            v[i] = reinterpret_cast<const uint4*>(tabs)[size_t(lm) * 6 + e % 5];
+        });
+    }
+    LDEV void store(uint32_t* dst) const {
+        static_for<0, int(PER)>([&](auto I) __attribute__((always_inline)) {
+            constexpr unsigned i = decltype(I)::value;
+            const unsigned e = threadIdx.x + i * NT;
+            if ((i + 1) * NT <= kVec || e < kVec) reinterpret_cast<uint4*>(dst)[e] = v[i];
+        });
+    }
+};
+
 // Workgroup-cooperative copy of N global FF8 tables (8-dword entries) into an
 // LdsTab8<N>, split so that the global loads are issued first (ahead of the
 // piece loads: vmcnt retires in order, so waiting for these does not wait for
@@ -402,7 +472,14 @@ LDEV unsigned skew_index(unsigned i, unsigned l) { return ((i >> l) | 1u) << l; 
 // LW: lanes per tile column strip (64 = a wave per column strip; 32 or 16 when
 // the lane groups of a wave hold different pieces: "w" is then the virtual wave
 // index (wave and lane group) and "lane" the lane inside its group).
-template <class F, int T, int R, int C, int LW = 64>
+//
+// S "split" bits: LDS exchanges (transposes, the formal derivative's wave-bit
+// gathers) run in 2^S rounds, one per value of tile bits [T-R, T-R+S), which
+// are register bits in both layouts of a two-layout tile; each round moves
+// 1/2^S of the tile through an area of 1/2^S the size.  This is what lets two
+// GF(2^16) workgroups of 256 pieces share a CU's 160 KiB of LDS, so that one
+// workgroup's loads and stores overlap the other's butterflies.
+template <class F, int T, int R, int C, int LW = 64, int S = 0>
 struct Tile {
     static_assert(R >= 1 && R <= T, "register bits");
     static constexpr int NR = 1 << R;         // pieces per lane
@@ -411,8 +488,22 @@ struct Tile {
     static constexpr int NL = (T + R - 1) / R;
     static constexpr int kLast = NL - 1;
     using Reg = uint32_t[NR][U];
+    static_assert(S == 0 || (NL == 2 && S <= 2 * R - T), "split bits must be register bits of both layouts");
+    static constexpr int kSB = T - R;  // first split bit
+    // LDS dwords of one exchange area (a transpose, a derivative gather)
+    static constexpr size_t kXchDwords = T > R ? (size_t(1) << (T - S)) * LW * U : 0;
+    // area slot of tile piece p: p without its split bits
+    LDEV static unsigned compact(unsigned p) {
+        if constexpr (S == 0) return p;
+        else return (p & ((1u << kSB) - 1)) | ((p >> (kSB + S)) << kSB);
+    }
+    // split bits of the piece register r holds in layout k (compile time: register bits)
+    static constexpr unsigned split_of(int k, int r) {
+        return S == 0 ? 0u : (unsigned(r) >> (kSB - (k * R < T - R ? k * R : T - R))) & ((1u << S) - 1);
+    }
 
     static constexpr int lo(int k) { return k * R < T - R ? k * R : T - R; }
+    static_assert(S == 0 || split_of(NL - 1, (1 << S) - 1) == (1u << S) - 1, "kLast: split class = low register bits");
     // IFFT layers done in layout k: [ifft_begin(k), lo(k) + R); FFT layers: [lo(k), fft_end(k))
     static constexpr int ifft_begin(int k) { return k == 0 ? 0 : lo(k - 1) + R; }
     static constexpr int fft_end(int k) { return k == NL - 1 ? T : lo(k + 1); }
@@ -492,6 +583,13 @@ struct Tile {
 #pragma unroll
                         for (int k = 0; k < F::kDw; ++k) b[k] ^= a[k];
                     }
+                    if constexpr (F::kDw == 2) {
+                        // GF(2^16): at most two butterflies in flight (each holds
+                        // ~10 temporaries next to a 64-VGPR tile and its table)
+#pragma unroll
+                        for (int k = 0; k < F::kDw; ++k) asm volatile("" : "+v"(a[k]), "+v"(b[k]));
+                        if ((j * C + u) & 1) __builtin_amdgcn_sched_barrier(0);
+                    }
                 }
             }
         };
@@ -526,11 +624,23 @@ struct Tile {
                 __builtin_amdgcn_sched_barrier(0);
             });
 #else
-            // FF16 (20-dword tables in SGPRs): one table live at a time, read
-            // inside the live branch (a second live table spilled SGPRs).
+            // FF16 (20-dword tables): one table live at a time, read inside the
+            // live branch; the scheduling barrier keeps the compiler from
+            // hoisting later groups' table reads (20 VGPRs each) next to a
+            // tile that already holds 64.
             static_for<0, NG>([&](auto GI) {
                 constexpr int g = decltype(GI)::value * 2 * half;
-                if (live(g)) group(g, table(g));
+                asm volatile("" ::: "memory");
+                if (live(g)) {
+                    group(g, table(g));
+                    // materialise the group's outputs here: otherwise the
+                    // arithmetic sinks to its next use and the table stays live
+#pragma unroll
+                    for (int j = 0; j < 2 * half; ++j)
+#pragma unroll
+                        for (int k = 0; k < U; ++k) asm volatile("" : "+v"(x[g + j][k]));
+                }
+                __builtin_amdgcn_sched_barrier(0);
             });
 #endif
         }
@@ -560,28 +670,48 @@ struct Tile {
                 F::muladd(a, b, t);
 #pragma unroll
                 for (int k = 0; k < F::kDw; ++k) b[k] ^= a[k];
+                if constexpr (F::kDw == 2) {  // as in layer(): bounded butterflies in flight
+#pragma unroll
+                    for (int k = 0; k < F::kDw; ++k) asm volatile("" : "+v"(a[k]), "+v"(b[k]));
+                    if ((r * C + u) & 1) __builtin_amdgcn_sched_barrier(0);
+                }
             }
         }
     }
 
-    // Move the tile from layout FROM to layout TO through LDS (2^T * 64 * U dwords).
+    // Move the tile from layout FROM to layout TO through LDS (kXchDwords; in
+    // 2^S rounds when split).  The rounds read into a second array: a round's
+    // TO registers are not the FROM registers written so far (the split bits
+    // are different register bits in the two layouts), so reading in place
+    // would overwrite values still to be written.  Register allocation turns
+    // the copy into renaming: a FROM value dies as it is written, so about one
+    // tile stays live.
     template <int FROM, int TO>
     LDEV static void transpose(Reg& x, unsigned w, unsigned lane, uint32_t* lds) {
         if constexpr ((LAMD_ABLATE & 2) != 0) return;
-        __syncthreads();
+        Reg y;
+        static_for<0, (1 << S)>([&](auto Q) {
+            constexpr unsigned q = decltype(Q)::value;
+            __syncthreads();
+            static_for<0, NR>([&](auto RI) {
+                constexpr int r = decltype(RI)::value;
+                if constexpr (split_of(FROM, r) == q) {
+                    uint32_t* p = lds + (size_t(compact(piece(FROM, r, w))) * LW + lane) * U;
 #pragma unroll
-        for (int r = 0; r < NR; ++r) {
-            uint32_t* p = lds + (size_t(piece(FROM, r, w)) * LW + lane) * U;
+                    for (int k = 0; k < U; ++k) p[k] = x[r][k];
+                }
+            });
+            __syncthreads();
+            static_for<0, NR>([&](auto RI) {
+                constexpr int r = decltype(RI)::value;
+                if constexpr (split_of(TO, r) == q) {
+                    const uint32_t* p = lds + (size_t(compact(piece(TO, r, w))) * LW + lane) * U;
 #pragma unroll
-            for (int k = 0; k < U; ++k) p[k] = x[r][k];
-        }
-        __syncthreads();
-#pragma unroll
-        for (int r = 0; r < NR; ++r) {
-            const uint32_t* p = lds + (size_t(piece(TO, r, w)) * LW + lane) * U;
-#pragma unroll
-            for (int k = 0; k < U; ++k) x[r][k] = p[k];
-        }
+                    for (int k = 0; k < U; ++k) y[r][k] = p[k];
+                }
+            });
+        });
+        copy(x, y);
     }
 
     // ------------------------------------------------------------------
@@ -678,6 +808,7 @@ struct Tile {
     // Transpose from layout FROM to layout TO through the ring's next area.
     template <int FROM, int TO, class Ring>
     LDEV static void exchange(Reg& x, unsigned w, unsigned lane, Ring& ring) {
+        static_assert(S == 0, "pipelined exchanges move the whole tile");
         uint32_t* area = ring.next();
         if constexpr ((LAMD_ABLATE & 2) != 0) return;
         if constexpr (Ring::kPreBarrier) __syncthreads();
@@ -702,8 +833,8 @@ struct Tile {
         constexpr int NS = kSkipTop ? T - 1 : T;  // layers computed here
         Look cur, nxt;
         if constexpr (NS > 0) read_look<ifft_layout(0), 0>(cur, w, ps, win, pred);
-        static_for<0, (NS > 0 ? NS : 0)>([&](auto S) {
-            constexpr int L = decltype(S)::value, k = ifft_layout(L);
+        static_for<0, (NS > 0 ? NS : 0)>([&](auto LI) {
+            constexpr int L = decltype(LI)::value, k = ifft_layout(L);
             const uint32_t live = live_mask<k, L>(cur, w, ps, pred);
             if constexpr (L + 1 < NS) read_look<ifft_layout(L + 1), L + 1>(nxt, w, ps, win, pred);
             apply<true, k, L>(x, cur, live);
@@ -721,8 +852,8 @@ struct Tile {
             if constexpr (fft_layout(top) != kLast) exchange<kLast, fft_layout(top)>(x, w, lane, ring);
             Look cur, nxt;
             read_look<fft_layout(top), top>(cur, w, ps, win, pred);
-            static_for<0, top + 1>([&](auto S) {
-                constexpr int L = top - decltype(S)::value, k = fft_layout(L);
+            static_for<0, top + 1>([&](auto LI) {
+                constexpr int L = top - decltype(LI)::value, k = fft_layout(L);
                 const uint32_t live = live_mask<k, L>(cur, w, ps, pred);
                 if constexpr (L > 0) read_look<fft_layout(L - 1), L - 1>(nxt, w, ps, win, pred);
                 apply<false, k, L>(x, cur, live);
@@ -732,44 +863,6 @@ struct Tile {
             if constexpr (fft_layout(0) != 0) exchange<fft_layout(0), 0>(x, w, lane, ring);
         } else if constexpr (NL > 1) {
             exchange<kLast, 0>(x, w, lane, ring);
-        }
-    }
-
-    // v = (I + D) v in layout kLast through the ring's next area (one barrier
-    // with two areas).  Register bits: ascending r reads v[r | 2^b] before it
-    // is modified; wave bits: gathered from the LDS copy of the original v.
-    template <class Ring>
-    LDEV static void derivative_ring(Reg& v, unsigned w, unsigned lane, Ring& ring) {
-        uint32_t* area = ring.next();
-        if constexpr ((LAMD_ABLATE & 64) != 0) return;
-        if constexpr (T > R) {
-            if constexpr (Ring::kPreBarrier) __syncthreads();
-#pragma unroll
-            for (int r = 0; r < NR; ++r) {
-                uint32_t* p = area + (size_t(piece(kLast, r, w)) * LW + lane) * U;
-#pragma unroll
-                for (int k = 0; k < U; ++k) p[k] = v[r][k];
-            }
-        }
-#pragma unroll
-        for (int r = 0; r < NR; ++r)
-#pragma unroll
-            for (int b = 0; b < R; ++b)
-                if (!(r & (1 << b)))
-#pragma unroll
-                    for (int k = 0; k < U; ++k) v[r][k] ^= v[r | (1 << b)][k];
-        if constexpr (T > R) {
-            __syncthreads();
-            for (int b = 0; b < T - R; ++b) {
-                if (w & (1u << b)) continue;  // wave-uniform
-                const unsigned w2 = w | (1u << b);
-#pragma unroll
-                for (int r = 0; r < NR; ++r) {
-                    const uint32_t* p = area + (size_t(piece(kLast, r, w2)) * LW + lane) * U;
-#pragma unroll
-                    for (int k = 0; k < U; ++k) v[r][k] ^= p[k];
-                }
-            }
         }
     }
 
@@ -812,115 +905,114 @@ struct Tile {
     // This computes v <- swap_top(v) + D_low(v) in layout kLast after an IFFT
     // without its top layer; the FFT then skips its top layer as well.
     // `area`: LDS for the wave-bit terms; pre_barrier: wait for earlier reads.
+    // In place, with the exchange split into rounds: round q handles the
+    // registers of split class q (ascending q, ascending r inside a class, the
+    // pairs (r, r + H) across the top bit together), so every register a term
+    // reads is still unmodified: the register terms of class q read classes
+    // >= q and higher registers of its own class; the wave-bit terms read the
+    // partner waves' originals that round q published in LDS first.
     LDEV static void derivative_swaptop(Reg& v, unsigned w, unsigned lane, uint32_t* area, bool pre_barrier) {
         if constexpr ((LAMD_ABLATE & 64) != 0) return;
         constexpr int H = NR / 2;  // register bit of the top tile bit (kLast holds the top R bits)
-        if constexpr (T > R) {
-            if (pre_barrier) __syncthreads();
+        static_for<0, (1 << S)>([&](auto Q) {
+            constexpr unsigned q = decltype(Q)::value;
+            if constexpr (T > R) {
+                if (pre_barrier || q > 0) __syncthreads();
+                static_for<0, NR>([&](auto RI) {
+                    constexpr int r = decltype(RI)::value;
+                    if constexpr (split_of(kLast, r) == q) {
+                        uint32_t* p = area + (size_t(compact(piece(kLast, r, w))) * LW + lane) * U;
 #pragma unroll
-            for (int r = 0; r < NR; ++r) {
-                uint32_t* p = area + (size_t(piece(kLast, r, w)) * LW + lane) * U;
-#pragma unroll
-                for (int k = 0; k < U; ++k) p[k] = v[r][k];
+                        for (int k = 0; k < U; ++k) p[k] = v[r][k];
+                    }
+                });
+                __syncthreads();
             }
-        }
-        Reg o;
-        copy(o, v);
+            static_for<0, H>([&](auto RI) {
+                constexpr int r = decltype(RI)::value;
+                if constexpr (split_of(kLast, r) == q) {
+                    uint32_t lo[U], hi[U];
 #pragma unroll
-        for (int r = 0; r < NR; ++r) {
+                    for (int k = 0; k < U; ++k) {
+                        lo[k] = v[r + H][k];
+                        hi[k] = v[r][k];
+                    }
 #pragma unroll
-            for (int k = 0; k < U; ++k) v[r][k] = o[r ^ H][k];
+                    for (int b = 0; b + 1 < R; ++b)
+                        if (!(r & (1 << b)))
 #pragma unroll
-            for (int b = 0; b + 1 < R; ++b)
-                if (!(r & (1 << b)))
+                            for (int k = 0; k < U; ++k) {
+                                lo[k] ^= v[r | (1 << b)][k];
+                                hi[k] ^= v[(r + H) | (1 << b)][k];
+                            }
 #pragma unroll
-                    for (int k = 0; k < U; ++k) v[r][k] ^= o[r | (1 << b)][k];
-        }
-        if constexpr (T > R) {
-            __syncthreads();
-            for (int b = 0; b < T - R; ++b) {
-                if (w & (1u << b)) continue;  // wave-uniform
-                const unsigned w2 = w | (1u << b);
+                    for (int k = 0; k < U; ++k) {
+                        v[r][k] = lo[k];
+                        v[r + H][k] = hi[k];
+                    }
+                }
+            });
+            if constexpr (T > R) {
+                for (int b = 0; b < T - R; ++b) {
+                    if (w & (1u << b)) continue;  // wave-uniform
+                    const unsigned w2 = w | (1u << b);
+                    static_for<0, NR>([&](auto RI) {
+                        constexpr int r = decltype(RI)::value;
+                        if constexpr (split_of(kLast, r) == q) {
+                            const uint32_t* p = area + (size_t(compact(piece(kLast, r, w2))) * LW + lane) * U;
 #pragma unroll
-                for (int r = 0; r < NR; ++r) {
-                    const uint32_t* p = area + (size_t(piece(kLast, r, w2)) * LW + lane) * U;
-#pragma unroll
-                    for (int k = 0; k < U; ++k) v[r][k] ^= p[k];
+                            for (int k = 0; k < U; ++k) v[r][k] ^= p[k];
+                        }
+                    });
                 }
             }
-        }
-    }
-
-    // v = (I + D) v in place: the derivative of a transform that fits the tile
-    // (layout kLast).  Register bits: ascending r reads v[r | 2^b] before it is
-    // modified; wave bits: gathered from an LDS copy of the original v.
-    LDEV static void derivative_inplace(Reg& v, unsigned w, unsigned lane, uint32_t* lds) {
-        if constexpr ((LAMD_ABLATE & 64) != 0) return;
-        if constexpr (T > R) {
-            __syncthreads();
-#pragma unroll
-            for (int r = 0; r < NR; ++r) {
-                uint32_t* p = lds + (size_t(piece(kLast, r, w)) * LW + lane) * U;
-#pragma unroll
-                for (int k = 0; k < U; ++k) p[k] = v[r][k];
-            }
-        }
-#pragma unroll
-        for (int r = 0; r < NR; ++r)
-#pragma unroll
-            for (int b = 0; b < R; ++b)
-                if (!(r & (1 << b)))
-#pragma unroll
-                    for (int k = 0; k < U; ++k) v[r][k] ^= v[r | (1 << b)][k];
-        if constexpr (T > R) {
-            __syncthreads();
-            for (int b = 0; b < T - R; ++b) {
-                if (w & (1u << b)) continue;  // wave-uniform
-                const unsigned w2 = w | (1u << b);
-#pragma unroll
-                for (int r = 0; r < NR; ++r) {
-                    const uint32_t* p = lds + (size_t(piece(kLast, r, w2)) * LW + lane) * U;
-#pragma unroll
-                    for (int k = 0; k < U; ++k) v[r][k] ^= p[k];
-                }
-            }
-        }
+        });
     }
 
     // d += sum over tile bits b with bit b of k clear of v[k | 2^b]   (layout kLast,
     // whose registers hold the top R bits and whose wave index is bits [0, T-R)).
-    // This is the tile's share of Leopard's formal derivative; with d = v it is
-    // the whole derivative of a transform that fits the tile (closed form of
+    // This is the tile's share of Leopard's formal derivative (closed form of
     // the loop at LeopardFF8.cpp:1890-1899: every source is read before it is
-    // modified, so out[k] = v[k] ^ XOR_{b: k_b = 0} v[k | 2^b]).
-    LDEV static void derivative_add(Reg& d, const Reg& v, unsigned w, unsigned lane, uint32_t* lds) {
+    // modified, so out[k] = v[k] ^ XOR_{b: k_b = 0} v[k | 2^b]).  v is not held
+    // as a tile: load(r, out) fetches register r of it, one split class at a
+    // time (8 pieces a round at S = 2), so d plus one class fits the VGPR budget.
+    template <class LoadFn>
+    LDEV static void derivative_add(Reg& d, LoadFn load, unsigned w, unsigned lane, uint32_t* lds) {
+        constexpr int NB = NR >> S;  // registers per class: class q = {r : r & (2^S - 1) = q}
+        static_for<0, (1 << S)>([&](auto Q) {
+            constexpr unsigned q = decltype(Q)::value;
+            uint32_t v[NB][U];
+            static_for<0, NB>([&](auto I) { load(int(I.value << S | q), v[I.value]); });
+            // register terms: v[r'] feeds d[r' - 2^b] for every register bit b set in r'
+            static_for<0, NB>([&](auto I) {
+                constexpr int rs = int(I.value << S | q);
 #pragma unroll
-        for (int r = 0; r < NR; ++r)
+                for (int b = 0; b < R; ++b)
+                    if (rs & (1 << b))
 #pragma unroll
-            for (int b = 0; b < R; ++b)
-                if (!(r & (1 << b)))
+                        for (int k = 0; k < U; ++k) d[rs ^ (1 << b)][k] ^= v[I.value][k];
+            });
+            if constexpr (T > R) {
+                __syncthreads();
+                static_for<0, NB>([&](auto I) {
+                    constexpr int r = int(I.value << S | q);
+                    uint32_t* p = lds + (size_t(compact(piece(kLast, r, w))) * LW + lane) * U;
 #pragma unroll
-                    for (int k = 0; k < U; ++k) d[r][k] ^= v[r | (1 << b)][k];
-        if constexpr (T > R) {
-            __syncthreads();
+                    for (int k = 0; k < U; ++k) p[k] = v[I.value][k];
+                });
+                __syncthreads();
+                for (int b = 0; b < T - R; ++b) {
+                    if (w & (1u << b)) continue;  // wave-uniform
+                    const unsigned w2 = w | (1u << b);
+                    static_for<0, NB>([&](auto I) {
+                        constexpr int r = int(I.value << S | q);
+                        const uint32_t* p = lds + (size_t(compact(piece(kLast, r, w2))) * LW + lane) * U;
 #pragma unroll
-            for (int r = 0; r < NR; ++r) {
-                uint32_t* p = lds + (size_t(piece(kLast, r, w)) * LW + lane) * U;
-#pragma unroll
-                for (int k = 0; k < U; ++k) p[k] = v[r][k];
-            }
-            __syncthreads();
-            for (int b = 0; b < T - R; ++b) {
-                if (w & (1u << b)) continue;  // wave-uniform
-                const unsigned w2 = w | (1u << b);
-#pragma unroll
-                for (int r = 0; r < NR; ++r) {
-                    const uint32_t* p = lds + (size_t(piece(kLast, r, w2)) * LW + lane) * U;
-#pragma unroll
-                    for (int k = 0; k < U; ++k) d[r][k] ^= p[k];
+                        for (int k = 0; k < U; ++k) d[r][k] ^= p[k];
+                    });
                 }
             }
-        }
+        });
     }
 };
 

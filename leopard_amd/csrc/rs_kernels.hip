@@ -51,6 +51,40 @@ struct SkewTables {
 };
 LDEV uint64_t lane_units(unsigned lane) { return (uint64_t(blockIdx.x) * 64 + lane) * C; }
 
+// Column addressing of the multi-pass GF(2^16) kernels: workgroup x owns units
+// [64x, 64x + 64) = bytes [512x, 512x + 512) of every piece (a unit = the low
+// and the high dword of 4 ALTMAP elements, 32 bytes apart).  The strip base is
+// wave-uniform and the lane's offset inside it a 32-bit VGPR, so each piece
+// access is a global_load/store with an SGPR base: no 64-bit vector address
+// per piece (32 pieces a lane).  Lanes past the last unit re-read the last
+// valid unit and never store.
+struct Cols16 {
+    uint64_t strip;  // byte offset of the strip (wave-uniform)
+    uint32_t off;    // this lane's byte offset inside the strip
+    bool live;
+};
+LDEV Cols16 cols16(uint64_t nunits, unsigned lane) {
+    const uint64_t first = uint64_t(blockIdx.x) * 64;
+    const uint64_t left = nunits - first;
+    const unsigned l = lane < left ? lane : unsigned(left - 1);
+    return Cols16{first * 8, (l >> 3) * 64u + (l & 7u) * 4u, lane < left};
+}
+// base: wave-uniform address of the strip (piece pointer + strip, or the zero page)
+LDEV void ld16(uint32_t* x, const uint8_t* base, uint32_t off) {
+    x[0] = *gptr<const uint32_t>(base + off);
+    x[1] = *gptr<const uint32_t>(base + off + 32);
+}
+LDEV void st16(uint8_t* base, uint32_t off, const uint32_t* x) {
+    *gptr<uint32_t>(base + off) = x[0];
+    *gptr<uint32_t>(base + off + 32) = x[1];
+}
+// piece i of pm when `ok` (wave-uniform), else zeros from the zero page
+LDEV void ld16z(uint32_t* x, const PieceMap& pm, bool ok, unsigned i, const uint8_t* zeros, const Cols16& c) {
+    const uint8_t* base = zeros;
+    if (ok) base = pm.ptr(i) + c.strip;
+    ld16(x, base, c.off);
+}
+
 // Piece i of pm when `ok` (wave-uniform), else zeros read from the zero page.
 // The choice is made on scalars so the vector code has no branch.
 template <class F>
@@ -112,105 +146,198 @@ __global__ void __launch_bounds__(64 << wave_bits(T), 4) k_enc_fused(EncArgs a) 
     }
 }
 
+// ------------------------------------------------- multi-pass GF(2^16) tiles --
+//
+// Tiles of the multi-pass transforms: 2^T pieces, 32 pieces per lane in
+// registers (R = 5), so a 256-piece tile is 8 waves and its LDS exchanges run
+// in 4 rounds through a 32 KiB area (Tile S = 2); with its butterfly tables
+// (and the decoder's per-piece scale / reveal tables) staged in LDS that is at
+// most 72 KiB, so two workgroups share every CU and one's loads and stores
+// overlap the other's butterflies (one 1024-thread, 128 KiB workgroup per CU
+// ran load -> butterflies -> store with nothing to overlap: ~35% VALU issue).
+constexpr int reg16(int T) { return T <= 5 ? T : 5; }
+#ifndef LAMD_SPLIT16
+#define LAMD_SPLIT16 2
+#endif
+constexpr int split16(int T) { return T >= 7 ? LAMD_SPLIT16 : (T == 6 && LAMD_SPLIT16 ? 1 : 0); }
+// the multi-chunk encoder pass keeps an accumulator tile as well: 16 pieces per lane
+constexpr int reg16_acc(int T) { return T <= 4 ? T : 4; }
+constexpr int split16_acc(int T) { return T == 6 ? 1 : 0; }
+constexpr unsigned threads16(int T, int R) { return 64u << (T - R); }
+
+template <int T, int R, int S>
+using Tile16 = Tile<FF16, T, R, C, 64, S>;
+
+// Pruning inside a multi-pass tile: off by default.  A per-group branch around
+// updates of a 64-VGPR tile makes the register allocator copy and spill at
+// every merge; every butterfly runs instead (a dead IFFT block is all zero and
+// stays zero, a dead FFT block feeds no needed output, so results are the
+// same).  Whole tiles are still skipped: the lo passes run only tiles with
+// input, the hi passes read zeros for empty low tiles, k_dec_fin returns on
+// tiles without a lost original.  LAMD_PRUNE16=1 builds the per-group form.
+#ifndef LAMD_PRUNE16
+#define LAMD_PRUNE16 0
+#endif
+template <class P>
+LDEV auto prune16(const P& p) {
+    if constexpr (LAMD_PRUNE16 != 0) return p;
+    else return AllLive{};
+}
+
+// LDS carve-up: exchange area, then `sets` butterfly-table sets, then `logs`
+// per-piece log-value table slots.
+template <int T, int R, int S>
+constexpr size_t lds16_dwords(int sets, int logs) {
+    return Tile16<T, R, S>::kXchDwords + size_t(sets) * (size_t(1) << T) * kTab16LdsDwords +
+           size_t(logs) * kTab16LdsDwords;
+}
+
+// x[r] ^= the units of piece map pm at tile pieces piece(LAY, r, w), loaded in
+// batches of 8 pieces (keeps the batch's VGPRs bounded next to a full tile).
+template <class TL, int LAY, class PosFn>
+LDEV void xor_load(typename TL::Reg& x, const PieceMap& pm, PosFn pos, unsigned w, const Cols16& cl) {
+    constexpr int B = TL::NR < 8 ? TL::NR : 8;
+    static_for<0, TL::NR / B>([&](auto BI) {
+        constexpr int r0 = decltype(BI)::value * B;
+        uint32_t y[B][TL::U];
+        static_for<0, B>([&](auto I) { ld16(y[I.value], pm.ptr(pos(TL::piece(LAY, r0 + I.value, w))) + cl.strip, cl.off); });
+        static_for<0, B>([&](auto I) {
+#pragma unroll
+            for (int k = 0; k < TL::U; ++k) x[r0 + I.value][k] ^= y[I.value][k];
+        });
+    });
+}
+
 // pass 1: IFFT over the low kLoBits of chunk blockIdx.z -> slab_out[c*m + g]
-template <class F>
-__global__ void __launch_bounds__(64 << wave_bits(kLoBits), 4) k_enc_lo(EncArgs a) {
+// (tables: skew base m-1 + c*m, the tile's positions y*256 + j)
+template <int R, int S>
+__global__ void __launch_bounds__(threads16(kLoBits, R), 4) k_enc_lo(EncArgs a) {
     constexpr int T = kLoBits;
-    using TL = Tile<F, T, reg_bits(T), C>;
+    constexpr int NT = threads16(T, R);
+    using TL = Tile16<T, R, S>;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    GlobalWindow<F> win;
+    uint32_t* set = lds + TL::kXchDwords;
     const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const uint64_t q0 = lane_units(lane);
-    const bool live = q0 < a.nunits;
-    const uint64_t ql = live ? q0 : a.nunits - C;
+    const Cols16 cl = cols16(a.nunits, lane);
+    const bool live = cl.live;
     const unsigned m = 1u << a.Tm;
-    const unsigned c = blockIdx.z, base = c * m;
-    const PieceSpace ps{0, 0, blockIdx.y << T};
+    const unsigned c = blockIdx.z, base = c * m, y = blockIdx.y;
+    const PieceSpace ps{0, 0, y << T};
+    Tabs16Stage<NT, T> st;
+    st.load(a.sktab, int(m - 1 + base), y << T, 0);
     typename TL::Reg x;
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) {
         const unsigned g = ps.global(TL::piece(0, r, w));
-        load_or_zero<F>(x[r], a.in, base + g < a.K, base + g, a.zeros, ql);
+        ld16z(x[r], a.in, base + g < a.K, base + g, a.zeros, cl);
     }
-    win.stage(a.sktab, int(m - 1 + base));
-    TL::ifft(x, w, lane, lds, ps, win, BelowLive{a.K - base});
+    st.store(set);
+    __syncthreads();
+    TL::ifft(x, w, lane, lds, ps, LdsWindow16{set, y << T, 0}, prune16(BelowLive{a.K - base}));
     if (!live) return;
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) {
         const unsigned g = ps.global(TL::piece(TL::kLast, r, w));
-        store_units<F, C>(a.slab_out.ptr(base + g), q0, x[r]);
+        st16(a.slab_out.ptr(base + g) + cl.strip, cl.off, x[r]);
     }
 }
 
 // pass 2: for every chunk IFFT over the high bits and accumulate; then the
-// FFT over the high bits -> slab_out[g]
-template <class F, int T>
-__global__ void __launch_bounds__(64 << wave_bits(T), 4) k_enc_hi(EncArgs a) {
-    using TL = Tile<F, T, reg_bits(T), C>;
+// FFT over the high bits -> slab_out[g].  Tile positions y + (j << 8): the IFFT
+// tables of chunk c (skew base m-1 + c*m) and the FFT tables (base -1) are two
+// LDS sets.  kMulti: several chunks (T <= 6 then), accumulated in a second tile.
+template <int T, int R, int S, bool kMulti>
+__global__ void __launch_bounds__(threads16(T, R), 4) k_enc_hi(EncArgs a) {
+    constexpr int NT = threads16(T, R);
+    using TL = Tile16<T, R, S>;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    GlobalWindow<F> win;
+    uint32_t* iset = lds + TL::kXchDwords;
+    uint32_t* fset = iset + (size_t(1) << T) * kTab16LdsDwords;
     const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const uint64_t q0 = lane_units(lane);
-    const bool live = q0 < a.nunits;
-    const uint64_t ql = live ? q0 : a.nunits - C;
+    const Cols16 cl = cols16(a.nunits, lane);
+    const bool live = cl.live;
     const unsigned m = 1u << a.Tm;
     const PieceSpace ps{blockIdx.y, kLoBits, 0};
-    typename TL::Reg acc, x;
-    for (unsigned c = 0; c < a.nchunks; ++c) {
+    const LdsWindow16 iwin{iset, 0, kLoBits}, fwin{fset, 0, kLoBits};
+    typename TL::Reg x;
+    auto load_chunk = [&](unsigned c) {
         const unsigned base = c * m;
 #pragma unroll
         for (int r = 0; r < TL::NR; ++r) {
             const unsigned tp = TL::piece(0, r, w);
             // low tiles that lie entirely past K were all-zero inputs
-            load_or_zero<F>(x[r], a.slab_in, base + (tp << kLoBits) < a.K, base + ps.global(tp), a.zeros, ql);
+            ld16z(x[r], a.slab_in, base + (tp << kLoBits) < a.K, base + ps.global(tp), a.zeros, cl);
         }
-        win.stage(a.sktab, int(m - 1 + base));
-        TL::template ifft<true>(x, w, lane, lds, ps, win, BelowLive{a.K - base});
-        TL::fused_top(x, F::tab(a.tabs, cload(a.fused + c)));  // top of the m-transform: this pass's top bit
-        if (c == 0) TL::copy(acc, x);
-        else TL::xor_into(acc, x);
+    };
+    {
+        Tabs16Stage<NT, T> si, sf;
+        si.load(a.sktab, int(m - 1), 0, kLoBits);
+        sf.load(a.sktab, -1, 0, kLoBits);
+        load_chunk(0);
+        si.store(iset);
+        sf.store(fset);
+        __syncthreads();
     }
-    win.stage(a.sktab, -1);
-    TL::template fft<true>(acc, w, lane, lds, ps, win, BelowLive{a.R});
+    if constexpr (!kMulti) {
+        TL::template ifft<true>(x, w, lane, lds, ps, iwin, prune16(BelowLive{a.K}));
+        TL::fused_top(x, FF16::tab(a.tabs, cload(a.fused)));  // top of the m-transform: this pass's top bit
+    } else {
+        typename TL::Reg acc;
+        for (unsigned c = 0;;) {
+            TL::template ifft<true>(x, w, lane, lds, ps, iwin, prune16(BelowLive{a.K - c * m}));
+            TL::fused_top(x, FF16::tab(a.tabs, cload(a.fused + c)));
+            if (c == 0) TL::copy(acc, x);
+            else TL::xor_into(acc, x);
+            if (++c >= a.nchunks) break;
+            Tabs16Stage<NT, T> si;
+            si.load(a.sktab, int(m - 1 + c * m), 0, kLoBits);
+            load_chunk(c);
+            __syncthreads();  // every wave is done with the previous chunk's tables
+            si.store(iset);
+            __syncthreads();
+        }
+        TL::copy(x, acc);
+    }
+    TL::template fft<true>(x, w, lane, lds, ps, fwin, prune16(BelowLive{a.R}));
     if (!live) return;
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) {
         const unsigned g = ps.global(TL::piece(0, r, w));
-        store_units<F, C>(a.slab_out.ptr(g), q0, acc[r]);
+        st16(a.slab_out.ptr(g) + cl.strip, cl.off, x[r]);
     }
 }
 
 // pass 3: FFT over the low bits, keep outputs g < R.  When m = 2^kLoBits (no
 // high pass) the chunk IFFTs of pass 1 are combined here: x = XOR_c U[c*m + g].
-template <class F>
-__global__ void __launch_bounds__(64 << wave_bits(kLoBits), 4) k_enc_fin(EncArgs a) {
+template <int R, int S>
+__global__ void __launch_bounds__(threads16(kLoBits, R), 4) k_enc_fin(EncArgs a) {
     constexpr int T = kLoBits;
-    using TL = Tile<F, T, reg_bits(T), C>;
+    constexpr int NT = threads16(T, R);
+    using TL = Tile16<T, R, S>;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    GlobalWindow<F> win;
+    uint32_t* set = lds + TL::kXchDwords;
     const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const uint64_t q0 = lane_units(lane);
-    const bool live = q0 < a.nunits;
-    const uint64_t ql = live ? q0 : a.nunits - C;
-    const PieceSpace ps{0, 0, blockIdx.y << T};
+    const Cols16 cl = cols16(a.nunits, lane);
+    const bool live = cl.live;
+    const unsigned y = blockIdx.y;
+    const PieceSpace ps{0, 0, y << T};
+    Tabs16Stage<NT, T> st;
+    st.load(a.sktab, -1, y << T, 0);
     typename TL::Reg x;
+    auto pos = [&](unsigned tp) { return ps.global(tp); };
 #pragma unroll
-    for (int r = 0; r < TL::NR; ++r) load_units<F, C>(x[r], a.slab_in.ptr(ps.global(TL::piece(TL::kLast, r, w))), ql);
+    for (int r = 0; r < TL::NR; ++r) ld16(x[r], a.slab_in.ptr(pos(TL::piece(TL::kLast, r, w))) + cl.strip, cl.off);
+    st.store(set);
+    __syncthreads();
     if (a.Tm == unsigned(kLoBits))
-        for (unsigned c = 1; c < a.nchunks; ++c) {
-            typename TL::Reg y;
-#pragma unroll
-            for (int r = 0; r < TL::NR; ++r)
-                load_units<F, C>(y[r], a.slab_in.ptr((c << T) + ps.global(TL::piece(TL::kLast, r, w))), ql);
-            TL::xor_into(x, y);
-        }
-    win.stage(a.sktab, -1);
-    TL::fft(x, w, lane, lds, ps, win, BelowLive{a.R});
+        for (unsigned c = 1; c < a.nchunks; ++c)
+            xor_load<TL, TL::kLast>(x, a.slab_in, [&](unsigned tp) { return (c << T) + pos(tp); }, w, cl);
+    TL::fft(x, w, lane, lds, ps, LdsWindow16{set, y << T, 0}, prune16(BelowLive{a.R}));
     if (!live) return;
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) {
         const unsigned g = ps.global(TL::piece(0, r, w));
-        if (g < a.R) store_units<F, C>(a.out.ptr(g), q0, x[r]);
+        if (g < a.R) st16(a.out.ptr(g) + cl.strip, cl.off, x[r]);
     }
 }
 
@@ -228,108 +355,91 @@ struct Pyr16Live {
     }
 };
 
-// FF16 decoder state in device memory: erasure bitmap (bit p <=>
-// error_locations[p] = 1, LeopardFF8.cpp:1825-1840) and error locator logs.
-// Multiply tables by log value come through the scalar cache.
-struct State16 {
-    const uint32_t* bits;
-    const uint32_t* el;
-    const uint32_t* tabs;
-    LDEV bool erased(unsigned p) const { return bit_set(bits, p); }
-    LDEV unsigned loc(unsigned p) const { return cload(el + p); }
-    LDEV FF16::Tab table(unsigned lm) const { return FF16::tab(tabs, lm); }
-};
-
-// Received piece at codeword position p (to be scaled by exp(el[p])); zero if
+// Received piece at codeword position p (scaled later by exp(el[p])); zero if
 // absent.  Positions: [0, m) recovery (only [0, R) exist), [m, m+K) originals
 // (LeopardFF8.cpp:1857-1877).  Branch-free on the vector side: an absent piece
-// reads the zero page at unit 0 and is scaled through the all-zero table.
-// Returns the log of the scale factor.
-template <class F, class St>
-LDEV unsigned load_received(uint32_t* x, const DecArgs& a, const St& st, unsigned p, uint64_t q) {
-    const uint8_t* src = a.zeros;
-    unsigned lm = F::kModulus + 1;  // the zero table
-    uint64_t qq = 0;
-    if (!st.erased(p)) {
-        if (p < a.R) { src = a.rec.ptr(p); lm = st.loc(p); qq = q; }
-        else if (p >= a.m && p < a.m + a.K) { src = a.orig.ptr(p - a.m); lm = st.loc(p); qq = q; }
+// reads the zero page at unit 0.
+LDEV void load_received(uint32_t* x, const DecArgs& a, unsigned p, const Cols16& c) {
+    const uint8_t* base = a.zeros;
+    if (!bit_set(a.erased_dev, p)) {
+        if (p < a.R) base = a.rec.ptr(p) + c.strip;
+        else if (p >= a.m && p < a.m + a.K) base = a.orig.ptr(p - a.m) + c.strip;
     }
-    load_units<F, C>(x, src, qq);
-    return lm;
+    ld16(x, base, c.off);
 }
 
-// Lost original at position p = m + i: work[i] = z[p] * exp(-el[p])  (LeopardFF8.cpp:1913-1915).
-template <class F, class St>
-LDEV void reveal(const uint32_t* z, const DecArgs& a, const St& st, unsigned p, uint64_t q0) {
-    if (p >= a.m && p < a.m + a.K && st.erased(p)) {
-        uint32_t y[C * F::kDw];
-        const typename F::Tab t = st.table(F::kModulus - st.loc(p));
-#pragma unroll
-        for (int u = 0; u < C; ++u) F::mul(&y[u * F::kDw], &z[u * F::kDw], t);
-        store_units<F, C>(a.out.ptr(p - a.m), q0, y);
-    }
-}
-
-// pass 1: scale-on-load + IFFT over the low bits -> a_out[g]
-template <class F>
-__global__ void __launch_bounds__(64 << wave_bits(kLoBits), 4) k_dec_lo(DecArgs a) {
+// pass 1: scale-on-load + IFFT over the low bits -> a_out[g].  LDS: exchange
+// area, the tile's butterfly tables (skew base -1, positions y*256 + j), and
+// its 256 scale tables (log value scale_logs[p] = el[p], or the zero table).
+template <int R, int S>
+__global__ void __launch_bounds__(threads16(kLoBits, R), 4) k_dec_lo(DecArgs a) {
     constexpr int T = kLoBits;
-    using TL = Tile<F, T, reg_bits(T), C>;
+    constexpr int NT = threads16(T, R);
+    using TL = Tile16<T, R, S>;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    GlobalWindow<F> win;
+    uint32_t* set = lds + TL::kXchDwords;
+    uint32_t* scl = set + (size_t(1) << T) * kTab16LdsDwords;
     const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const uint64_t q0 = lane_units(lane);
-    const bool live = q0 < a.nunits;
-    const uint64_t ql = live ? q0 : a.nunits - C;
-    const PieceSpace ps{0, 0, blockIdx.y << T};
-    const State16 st{a.erased_dev, a.el, a.tabs};
+    const Cols16 cl = cols16(a.nunits, lane);
+    const bool live = cl.live;
+    const unsigned y = blockIdx.y;
+    const PieceSpace ps{0, 0, y << T};
+    Tabs16Stage<NT, T> st;
+    st.load(a.sktab, -1, y << T, 0);
+    LogTabs16Stage<NT, (1u << T)> ls;
+    ls.load(a.tabs, a.scale_logs + (y << T));
     typename TL::Reg v;
-    // every piece load in flight first, then the scale multiplies (one table
-    // live at a time)
-    unsigned lm[TL::NR];
 #pragma unroll
-    for (int r = 0; r < TL::NR; ++r) lm[r] = load_received<F>(v[r], a, st, ps.global(TL::piece(0, r, w)), ql);
+    for (int r = 0; r < TL::NR; ++r) load_received(v[r], a, ps.global(TL::piece(0, r, w)), cl);
+    st.store(set);
+    ls.store(scl);
+    __syncthreads();
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) {
-        const typename F::Tab t = st.table(lm[r]);
+        asm volatile("" ::: "memory");  // keeps the compiler from hoisting every table read up here
+        const FF16::Tab t = FF16::tab_lds(scl + TL::piece(0, r, w) * kTab16LdsDwords);
 #pragma unroll
-        for (int u = 0; u < C; ++u) F::mul(&v[r][u * F::kDw], &v[r][u * F::kDw], t);
-        __builtin_amdgcn_sched_barrier(0);
+        for (int u = 0; u < C; ++u) FF16::mul(&v[r][u * 2], &v[r][u * 2], t);
+#pragma unroll
+        for (int k = 0; k < 2 * C; ++k) asm volatile("" : "+v"(v[r][k]));  // one scale table live at a time
     }
-    win.stage(a.sktab, -1);
-    TL::ifft(v, w, lane, lds, ps, win, Pyr16Live{a.present_pyr});
+    TL::ifft(v, w, lane, lds, ps, LdsWindow16{set, y << T, 0}, prune16(Pyr16Live{a.present_pyr}));
     if (!live) return;
 #pragma unroll
-    for (int r = 0; r < TL::NR; ++r) store_units<F, C>(a.a_out.ptr(ps.global(TL::piece(TL::kLast, r, w))), q0, v[r]);
+    for (int r = 0; r < TL::NR; ++r) st16(a.a_out.ptr(ps.global(TL::piece(TL::kLast, r, w))) + cl.strip, cl.off, v[r]);
 }
 
 // pass 2: A = F_hi (I + D_hi) I_hi U over the high bits, computed as
 // F_hi' (swap_top + D_hi') I_hi' U without the top layers (Tile::derivative_swaptop).
 // The other term of the split derivative needs F_hi(I_hi U) = U, which pass 3
-// reads straight from pass 1's slab.
-template <class F, int T>
-__global__ void __launch_bounds__(64 << wave_bits(T), 4) k_dec_hi(DecArgs a) {
-    using TL = Tile<F, T, reg_bits(T), C>;
+// reads straight from pass 1's slab.  Tables: skew base -1, positions j << 8.
+template <int T, int R, int S>
+__global__ void __launch_bounds__(threads16(T, R), 4) k_dec_hi(DecArgs a) {
+    constexpr int NT = threads16(T, R);
+    using TL = Tile16<T, R, S>;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    GlobalWindow<F> win;
+    uint32_t* set = lds + TL::kXchDwords;
     const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const uint64_t q0 = lane_units(lane);
-    const bool live = q0 < a.nunits;
-    const uint64_t ql = live ? q0 : a.nunits - C;
+    const Cols16 cl = cols16(a.nunits, lane);
+    const bool live = cl.live;
     const PieceSpace ps{blockIdx.y, kLoBits, 0};
+    Tabs16Stage<NT, T> st;
+    st.load(a.sktab, -1, 0, kLoBits);
     typename TL::Reg v;
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) {
         const unsigned tp = TL::piece(0, r, w);
-        load_or_zero<F>(v[r], a.a_in, tp < a.nlo, ps.global(tp), a.zeros, ql);
+        ld16z(v[r], a.a_in, tp < a.nlo, ps.global(tp), a.zeros, cl);
     }
-    win.stage(a.sktab, -1);
-    TL::template ifft<true>(v, w, lane, lds, ps, win, Pyr16Live{a.present_pyr});
+    st.store(set);
+    __syncthreads();
+    const LdsWindow16 win{set, 0, kLoBits};
+    TL::template ifft<true>(v, w, lane, lds, ps, win, prune16(Pyr16Live{a.present_pyr}));
     TL::derivative_swaptop(v, w, lane, lds, true);
-    TL::template fft<true>(v, w, lane, lds, ps, win, Pyr16Live{a.needed_pyr});
+    TL::template fft<true>(v, w, lane, lds, ps, win, prune16(Pyr16Live{a.needed_pyr}));
     if (live)
 #pragma unroll
-        for (int r = 0; r < TL::NR; ++r) store_units<F, C>(a.a_out.ptr(ps.global(TL::piece(0, r, w))), q0, v[r]);
+        for (int r = 0; r < TL::NR; ++r) st16(a.a_out.ptr(ps.global(TL::piece(0, r, w))) + cl.strip, cl.off, v[r]);
 }
 
 // pass 2 when every received piece is in the low half (K = R, every original
@@ -337,66 +447,85 @@ __global__ void __launch_bounds__(64 << wave_bits(T), 4) k_dec_hi(DecArgs a) {
 // half, the fused top layer of the m-transform (encoder chunk 0's table) and the
 // high FFT layers with the skews of the high half; A is written at the high
 // positions only and pass 3 adds D_lo(U) = 0 there (U has no high tiles).
-template <class F, int T>
-__global__ void __launch_bounds__(64 << wave_bits(T), 4) k_dec_hi_half(DecArgs a) {
-    using TL = Tile<F, T, reg_bits(T), C>;
+// Tables: skew base -1, positions j << 8 (low half) and m + (j << 8) (high half).
+template <int T, int R, int S>
+__global__ void __launch_bounds__(threads16(T, R), 4) k_dec_hi_half(DecArgs a) {
+    constexpr int NT = threads16(T, R);
+    using TL = Tile16<T, R, S>;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    GlobalWindow<F> win;
+    uint32_t* lset = lds + TL::kXchDwords;
+    uint32_t* hset = lset + (size_t(1) << T) * kTab16LdsDwords;
     const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const uint64_t q0 = lane_units(lane);
-    const bool live = q0 < a.nunits;
-    const uint64_t ql = live ? q0 : a.nunits - C;
+    const Cols16 cl = cols16(a.nunits, lane);
+    const bool live = cl.live;
     const PieceSpace low{blockIdx.y, kLoBits, 0}, high{blockIdx.y, kLoBits, a.m};
+    Tabs16Stage<NT, T> sl, sh;
+    sl.load(a.sktab, -1, 0, kLoBits);
+    sh.load(a.sktab, -1, a.m, kLoBits);
     typename TL::Reg v;
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) {
         const unsigned tp = TL::piece(0, r, w);
-        load_or_zero<F>(v[r], a.a_in, tp < a.nlo, low.global(tp), a.zeros, ql);
+        ld16z(v[r], a.a_in, tp < a.nlo, low.global(tp), a.zeros, cl);
     }
-    win.stage(a.sktab, -1);
-    TL::template ifft<true>(v, w, lane, lds, low, win, Pyr16Live{a.present_pyr});
-    TL::fused_top(v, F::tab(a.tabs, cload(a.fused)));
-    TL::template fft<true>(v, w, lane, lds, high, win, Pyr16Live{a.needed_pyr});
+    sl.store(lset);
+    sh.store(hset);
+    __syncthreads();
+    TL::template ifft<true>(v, w, lane, lds, low, LdsWindow16{lset, 0, kLoBits}, prune16(Pyr16Live{a.present_pyr}));
+    TL::fused_top(v, FF16::tab(a.tabs, cload(a.fused)));
+    TL::template fft<true>(v, w, lane, lds, high, LdsWindow16{hset, a.m, kLoBits}, prune16(Pyr16Live{a.needed_pyr}));
     if (live)
 #pragma unroll
-        for (int r = 0; r < TL::NR; ++r) store_units<F, C>(a.a_out.ptr(high.global(TL::piece(0, r, w))), q0, v[r]);
+        for (int r = 0; r < TL::NR; ++r) st16(a.a_out.ptr(high.global(TL::piece(0, r, w))) + cl.strip, cl.off, v[r]);
 }
 
-// pass 3: z = A + D_lo(U), FFT over the low bits, reveal lost originals (U of
-// a low tile without received data is zero and was never written)
-template <class F>
-__global__ void __launch_bounds__(64 << wave_bits(kLoBits), 4) k_dec_fin(DecArgs a) {
+// pass 3: z = A + D_lo(U), FFT over the low bits, reveal lost originals
+// (work[i] = z[m + i] * exp(-el[m + i]), LeopardFF8.cpp:1913-1915; the reveal
+// tables, log value reveal_logs[p], staged in LDS).  U of a low tile without
+// received data is zero and was never written.
+template <int R, int S>
+__global__ void __launch_bounds__(threads16(kLoBits, R), 4) k_dec_fin(DecArgs a) {
     constexpr int T = kLoBits;
-    using TL = Tile<F, T, reg_bits(T), C>;
+    constexpr int NT = threads16(T, R);
+    using TL = Tile16<T, R, S>;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const unsigned y = blockIdx.y;
     // skip tiles holding no lost original (uniform across the workgroup)
-    {
-        const unsigned L = T, j = blockIdx.y;
-        if (!((cload(a.needed_pyr + pyr_offset(L) + (j >> 5)) >> (j & 31)) & 1u)) return;
-    }
-    GlobalWindow<F> win;
+    if (!((cload(a.needed_pyr + pyr_offset(T) + (y >> 5)) >> (y & 31)) & 1u)) return;
+    uint32_t* set = lds + TL::kXchDwords;
+    uint32_t* rvl = set + (size_t(1) << T) * kTab16LdsDwords;
     const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const uint64_t q0 = lane_units(lane);
-    const bool live = q0 < a.nunits;
-    const uint64_t ql = live ? q0 : a.nunits - C;
-    const PieceSpace ps{0, 0, blockIdx.y << T};
-    const State16 st{a.erased_dev, a.el, a.tabs};
+    const Cols16 cl = cols16(a.nunits, lane);
+    const bool live = cl.live;
+    const PieceSpace ps{0, 0, y << T};
+    Tabs16Stage<NT, T> st;
+    st.load(a.sktab, -1, y << T, 0);
+    LogTabs16Stage<NT, (1u << T)> ls;
+    ls.load(a.tabs, a.reveal_logs + (y << T));
     typename TL::Reg z;
 #pragma unroll
-    for (int r = 0; r < TL::NR; ++r) load_units<F, C>(z[r], a.a_in.ptr(ps.global(TL::piece(TL::kLast, r, w))), ql);
-    win.stage(a.sktab, -1);
+    for (int r = 0; r < TL::NR; ++r) ld16(z[r], a.a_in.ptr(ps.global(TL::piece(TL::kLast, r, w))) + cl.strip, cl.off);
+    st.store(set);
+    ls.store(rvl);
+    __syncthreads();
     // U of a tile past the received ones is zero, and so is D_lo(U) (workgroup-uniform)
-    if (blockIdx.y < a.nlo) {
-        typename TL::Reg v;
-#pragma unroll
-        for (int r = 0; r < TL::NR; ++r) load_units<F, C>(v[r], a.b_in.ptr(ps.global(TL::piece(TL::kLast, r, w))), ql);
-        TL::derivative_add(z, v, w, lane, lds);
-    }
-    TL::fft(z, w, lane, lds, ps, win, Pyr16Live{a.needed_pyr});
+    if (y < a.nlo)
+        TL::derivative_add(z, [&](int r, uint32_t* out) {
+            ld16(out, a.b_in.ptr(ps.global(TL::piece(TL::kLast, r, w))) + cl.strip, cl.off);
+        }, w, lane, lds);
+    TL::fft(z, w, lane, lds, ps, LdsWindow16{set, y << T, 0}, prune16(Pyr16Live{a.needed_pyr}));
     if (!live) return;
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) {
-        reveal<F>(z[r], a, st, ps.global(TL::piece(0, r, w)), q0);
+        const unsigned p = ps.global(TL::piece(0, r, w));
+        if (p >= a.m && p < a.m + a.K && bit_set(a.erased_dev, p)) {
+            uint32_t o[2 * C];
+            asm volatile("" ::: "memory");
+            const FF16::Tab t = FF16::tab_lds(rvl + TL::piece(0, r, w) * kTab16LdsDwords);
+#pragma unroll
+            for (int u = 0; u < C; ++u) FF16::mul(&o[u * 2], &z[r][u * 2], t);
+            st16(a.out.ptr(p - a.m) + cl.strip, cl.off, o);
+        }
         __builtin_amdgcn_sched_barrier(0);
     }
 }
@@ -421,8 +550,14 @@ LDEV void fwht256(unsigned (&e)[4], unsigned lane) {
     e[1] = Mod16::add(a1, a3); e[3] = Mod16::sub(a1, a3);
 }
 
-// mode 0: rows of the erasure bitmap -> tmp; mode 1: rows of tmp -> el (u16)
-__global__ void __launch_bounds__(64) k_el16_rows(const uint32_t* erased, uint32_t* tmp, uint32_t* el, int mode) {
+// mode 0: rows of the erasure bitmap -> tmp; mode 1: rows of tmp -> el, plus
+// the per-position log values of the decoder's multiplies: scale_logs[p] =
+// el[p] for a received piece (LeopardFF8.cpp:1857-1877), reveal_logs[p] =
+// kModulus - el[p] for a lost original (:1913-1915), the all-zero table
+// (65536) elsewhere.
+__global__ void __launch_bounds__(64) k_el16_rows(const uint32_t* erased, uint32_t* tmp, uint32_t* el,
+                                                 uint32_t* scale_logs, uint32_t* reveal_logs, int mode, unsigned m,
+                                                 unsigned K, unsigned R) {
     const unsigned lane = threadIdx.x, row = blockIdx.x;
     unsigned e[4];
 #pragma unroll
@@ -434,8 +569,15 @@ __global__ void __launch_bounds__(64) k_el16_rows(const uint32_t* erased, uint32
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const unsigned p = row * 256 + lane + 64 * j;
-        if (mode == 0) tmp[p] = e[j];
-        else el[p] = e[j];
+        if (mode == 0) {
+            tmp[p] = e[j];
+        } else {
+            el[p] = e[j];
+            const bool lost = bit_set(erased, p);
+            const bool orig = p >= m && p < m + K;
+            scale_logs[p] = !lost && (p < R || orig) ? e[j] : 65536u;
+            reveal_logs[p] = lost && orig ? 65535u - e[j] : 65536u;
+        }
     }
 }
 // columns: FWHT over the high bits, pointwise * LogWalsh mod 65535, FWHT again
@@ -496,76 +638,90 @@ struct EncFusedFn {
                       &a);
     }
 };
-template <class F, int T>
+template <int T, bool kMulti>
 struct EncHiFn {
     static hipError_t run(const EncArgs& a, hipStream_t s) {
-        return launch(&k_enc_hi<F, T>, dim3(tiles_for(a.nunits), 1u << kLoBits), 64u << wave_bits(T),
-                      full_tile_lds<F, T>(), s, &a);
+        constexpr int R = kMulti ? reg16_acc(T) : reg16(T), S = kMulti ? split16_acc(T) : split16(T);
+        return launch(&k_enc_hi<T, R, S, kMulti>, dim3(tiles_for(a.nunits), 1u << kLoBits), threads16(T, R),
+                      lds16_dwords<T, R, S>(2, 0), s, &a);
     }
 };
-template <class F, int T>
+template <int T>
 struct DecHiFn {
     static hipError_t run(const DecArgs& a, hipStream_t s) {
-        return launch(&k_dec_hi<F, T>, dim3(tiles_for(a.nunits), 1u << kLoBits), 64u << wave_bits(T),
-                      full_tile_lds<F, T>(), s, &a);
+        constexpr int R = reg16(T), S = split16(T);
+        return launch(&k_dec_hi<T, R, S>, dim3(tiles_for(a.nunits), 1u << kLoBits), threads16(T, R),
+                      lds16_dwords<T, R, S>(1, 0), s, &a);
     }
 };
-
-template <class F, int T>
+template <int T>
 struct DecHiHalfFn {
     static hipError_t run(const DecArgs& a, hipStream_t s) {
-        return launch(&k_dec_hi_half<F, T>, dim3(tiles_for(a.nunits), 1u << kLoBits), 64u << wave_bits(T),
-                      full_tile_lds<F, T>(), s, &a);
+        constexpr int R = reg16(T), S = split16(T);
+        return launch(&k_dec_hi_half<T, R, S>, dim3(tiles_for(a.nunits), 1u << kLoBits), threads16(T, R),
+                      lds16_dwords<T, R, S>(2, 0), s, &a);
     }
 };
 
-template <template <class, int> class Fn, class F, int TMIN, int TMAX, class A>
+template <template <int> class Fn, int TMIN, int TMAX, class A>
 hipError_t dispatch_T(unsigned T, const A& a, hipStream_t s) {
     hipError_t e = hipErrorInvalidValue;
     static_for<TMIN, TMAX + 1>([&](auto I) {
-        if (T == unsigned(decltype(I)::value)) e = Fn<F, decltype(I)::value>::run(a, s);
+        if (T == unsigned(decltype(I)::value)) e = Fn<decltype(I)::value>::run(a, s);
     });
     return e;
 }
+template <int T>
+using EncHiSingle = EncHiFn<T, false>;
+template <int T>
+using EncHiMulti = EncHiFn<T, true>;
+
+constexpr int kLoR = reg16(kLoBits), kLoS = split16(kLoBits);
 
 }  // namespace
 
 hipError_t launch_encode_fused16(unsigned T, const EncArgs& a, hipStream_t s) {
-    return dispatch_T<EncFusedFn, FF16, 1, 8>(T, a, s);
+    hipError_t e = hipErrorInvalidValue;
+    static_for<1, 9>([&](auto I) {
+        if (T == unsigned(decltype(I)::value)) e = EncFusedFn<FF16, decltype(I)::value>::run(a, s);
+    });
+    return e;
 }
 hipError_t launch_encode_lo(const EncArgs& a, hipStream_t s) {
     const unsigned m = 1u << a.Tm;
-    return launch(&k_enc_lo<FF16>, dim3(tiles_for(a.nunits), m >> kLoBits, a.nchunks), 64u << wave_bits(kLoBits),
-                  full_tile_lds<FF16, kLoBits>(), s, &a);
+    return launch(&k_enc_lo<kLoR, kLoS>, dim3(tiles_for(a.nunits), m >> kLoBits, a.nchunks),
+                  threads16(kLoBits, kLoR), lds16_dwords<kLoBits, kLoR, kLoS>(1, 0), s, &a);
 }
 hipError_t launch_encode_hi(const EncArgs& a, hipStream_t s) {
-    return dispatch_T<EncHiFn, FF16, 1, 8>(a.Tm - kLoBits, a, s);
+    if (a.nchunks > 1) return dispatch_T<EncHiMulti, 1, 6>(a.Tm - kLoBits, a, s);
+    return dispatch_T<EncHiSingle, 1, 7>(a.Tm - kLoBits, a, s);
 }
 hipError_t launch_encode_fin(const EncArgs& a, hipStream_t s) {
     const unsigned tiles = (a.R + (1u << kLoBits) - 1) >> kLoBits;
-    return launch(&k_enc_fin<FF16>, dim3(tiles_for(a.nunits), tiles), 64u << wave_bits(kLoBits),
-                  full_tile_lds<FF16, kLoBits>(), s, &a);
+    return launch(&k_enc_fin<kLoR, kLoS>, dim3(tiles_for(a.nunits), tiles), threads16(kLoBits, kLoR),
+                  lds16_dwords<kLoBits, kLoR, kLoS>(1, 0), s, &a);
 }
 hipError_t launch_decode_lo(const DecArgs& a, hipStream_t s) {
-    return launch(&k_dec_lo<FF16>, dim3(tiles_for(a.nunits), a.nlo), 64u << wave_bits(kLoBits),
-                  full_tile_lds<FF16, kLoBits>(), s, &a);
+    return launch(&k_dec_lo<kLoR, kLoS>, dim3(tiles_for(a.nunits), a.nlo), threads16(kLoBits, kLoR),
+                  lds16_dwords<kLoBits, kLoR, kLoS>(1, 1 << kLoBits), s, &a);
 }
 hipError_t launch_decode_hi(const DecArgs& a, hipStream_t s) {
-    return dispatch_T<DecHiFn, FF16, 1, 8>(a.Tn - kLoBits, a, s);
+    return dispatch_T<DecHiFn, 1, 8>(a.Tn - kLoBits, a, s);
 }
 hipError_t launch_decode_hi_half(const DecArgs& a, hipStream_t s) {
-    return dispatch_T<DecHiHalfFn, FF16, 1, 7>(a.Tn - 1 - kLoBits, a, s);
+    return dispatch_T<DecHiHalfFn, 1, 7>(a.Tn - 1 - kLoBits, a, s);
 }
 hipError_t launch_decode_fin(const DecArgs& a, hipStream_t s) {
     const unsigned n = 1u << a.Tn;
-    return launch(&k_dec_fin<FF16>, dim3(tiles_for(a.nunits), n >> kLoBits), 64u << wave_bits(kLoBits),
-                  full_tile_lds<FF16, kLoBits>(), s, &a);
+    return launch(&k_dec_fin<kLoR, kLoS>, dim3(tiles_for(a.nunits), n >> kLoBits), threads16(kLoBits, kLoR),
+                  lds16_dwords<kLoBits, kLoR, kLoS>(1, 1 << kLoBits), s, &a);
 }
 hipError_t launch_error_locator16(const uint32_t* erased, const uint32_t* walsh, uint32_t* tmp, uint32_t* el,
+                                  uint32_t* scale_logs, uint32_t* reveal_logs, unsigned m, unsigned K, unsigned R,
                                   hipStream_t s) {
-    hipLaunchKernelGGL(k_el16_rows, dim3(256), dim3(64), 0, s, erased, tmp, el, 0);
+    hipLaunchKernelGGL(k_el16_rows, dim3(256), dim3(64), 0, s, erased, tmp, el, scale_logs, reveal_logs, 0, m, K, R);
     hipLaunchKernelGGL(k_el16_cols, dim3(256), dim3(64), 0, s, tmp, walsh);
-    hipLaunchKernelGGL(k_el16_rows, dim3(256), dim3(64), 0, s, erased, tmp, el, 1);
+    hipLaunchKernelGGL(k_el16_rows, dim3(256), dim3(64), 0, s, erased, tmp, el, scale_logs, reveal_logs, 1, m, K, R);
     return hipGetLastError();
 }
 hipError_t launch_xor_reduce(const XorArgs& a, hipStream_t s) {

@@ -60,10 +60,15 @@ def key(*a):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--big", action="store_true", help="also digest the BASELINE shapes (needs ~10 GB RAM)")
+    ap.add_argument("--big-decode", action="store_true",
+                    help="only add the decoder digests at the BASELINE shapes to golden_digests.json")
     args = ap.parse_args()
     ref = ol.reference()
     if ref is None:
         sys.exit("build the reference first: make -C oracle ref")
+    if args.big_decode:
+        big_decode(ref)
+        return
 
     out = {}
     for (k, r, b) in SMALL_ENC:
@@ -100,6 +105,35 @@ def main():
             json.dump({"convention": "sha256 of recovery pieces 0..R-1 concatenated; inputs pcg_bytes(2,0,K,B) "
                                      "for 'digests', hash_bytes(7,K,B) for 'hash_digests'",
                        "digests": dig, "hash_digests": hdig}, f, indent=1)
+
+
+def big_decode(ref):
+    """Decoder digests at the BASELINE shapes on NON-codeword inputs (pins the
+    decoder's exact map at full size, not only its round trip): originals
+    hash_bytes(7, K, B), "recovery" pieces hash_bytes(8, R, B), the benchmark's
+    loss pattern with loss = R (benchmark_losses(K, R, R, seed=2, trial=0):
+    R originals lost, every recovery piece kept); digest = sha256 of the
+    rebuilt originals concatenated in loss order."""
+    path = os.path.join(HERE, "golden_digests.json")
+    with open(path) as f:
+        doc = json.load(f)
+    dd = doc.setdefault("decode_hash_digests", {})
+    for (k, r, b) in BIG:
+        d = ol.hash_bytes(7, k, b)
+        rec = ol.hash_bytes(8, r, b)
+        lo, lr = ol.benchmark_losses(k, r, r, seed=2, trial=0)
+        res = ref.decode(d, rec, lo, lr)
+        h = hashlib.sha256()
+        for i in lo:
+            h.update(res[i].tobytes())
+        dd[key(k, r, b)] = h.hexdigest()
+        print("big-decode", k, r, b, dd[key(k, r, b)], flush=True)
+        del d, rec, res
+    doc["decode_convention"] = ("decode_hash_digests: sha256 of the lost originals (benchmark_losses(K, R, R, seed=2, "
+                                "trial=0) order) rebuilt from originals hash_bytes(7,K,B) and non-codeword recovery "
+                                "pieces hash_bytes(8,R,B)")
+    with open(path, "w") as f:
+        json.dump(doc, f, indent=1)
 
 
 if __name__ == "__main__":

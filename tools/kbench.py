@@ -12,7 +12,8 @@ import leopard_amd as leo  # noqa: E402
 from bench import hash_fill_cuda  # noqa: E402
 
 
-def run(k, r, b, sets=16, n=100, warm=int(os.environ.get('KB_WARM', '300'))):
+def run(k, r, b, sets=int(os.environ.get('KB_SETS', '16')), n=int(os.environ.get('KB_N', '100')),
+        warm=int(os.environ.get('KB_WARM', '300'))):
     VP = ctypes.c_void_p
     lib = leo.lib
     ewc, dwc = leo.leo_encode_work_count(k, r), leo.leo_decode_work_count(k, r)

@@ -15,7 +15,8 @@ def main():
                 name = row["Kernel_Name"]
                 if "lamd" not in name:
                     continue
-                short = name.split("::")[-1][:60]
+                short = name.replace("lamd::(anonymous namespace)::", "").replace("lamd::", "").split("(")[0][:60]
+                short += f"  grid={row.get('Grid_Size', '')}"
                 agg[short][row["Counter_Name"]].append(float(row["Counter_Value"]))
     for k, cs in agg.items():
         print(k)

@@ -15,15 +15,23 @@ import oracle_lib as ol  # noqa: E402
 
 
 def main():
-    k, r, b, loss = (int(x) for x in sys.argv[1:5])
-    seed = int(sys.argv[5]) if len(sys.argv) > 5 else 1
     assert leo.leo_init() == 0
+    args = sys.argv[1:]
+    for i in range(0, len(args), 4):
+        case(*(int(x) for x in args[i:i + 4]))
+
+
+def case(k, r, b, loss, seed=1):
     rng = np.random.default_rng(seed)
     data = rng.integers(0, 256, (k, b), dtype=np.uint8)
     rec = ol.oracle().encode(data, r)
     dt = torch.from_numpy(data).cuda()
     got_rec = leo.encode(dt, r).cpu().numpy()
     enc_ok = np.array_equal(got_rec, rec)
+    if not enc_ok:
+        rows = [i for i in range(r) if not np.array_equal(got_rec[i], rec[i])]
+        cols = sorted(set(np.nonzero((got_rec != rec).any(axis=0))[0].tolist()))
+        print(f"  encode bad rows {len(rows)}: {rows[:40]} ... bad cols {len(cols)}: {cols[:32]}")
     lo = sorted(rng.choice(k, loss, replace=False).tolist())
     lr = sorted(rng.choice(r, r - loss, replace=False).tolist())
     try:
@@ -34,6 +42,9 @@ def main():
     except Exception as e:  # noqa: BLE001
         print(f"case {k} {r} {b} {loss}: enc_ok={enc_ok} decode error {e}")
         sys.exit(3)
+    if bad:
+        d = res[bad[0]].cpu().numpy() != data[bad[0]]
+        print(f"  first bad piece {bad[0]}: bad cols {np.nonzero(d)[0][:32].tolist()}")
 
 
 if __name__ == "__main__":

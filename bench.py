@@ -1,33 +1,41 @@
 #!/usr/bin/env python3
 """Benchmark: device-resident Leopard-RS encode + decode through the C ABI.
 
-Metric (BASELINE.json): device-resident encode+decode GB/s of input bytes.
-One *step* = one leo_encode of a batch plus one worst-case leo_decode of the
-same batch (every original lost, decoded from the R recovery pieces), both
-called through the drop-in C ABI with device pointers, in async mode.  Step s
-runs on HIP stream s % S (--streams, default 3 objects in flight: a single
-64 KiB-piece call fills each CU with one workgroup, and concurrent objects
-fill the phases where one call waits on memory or barriers); the same steps on
-one stream are reported as "serial".  value = (input bytes K*B per step,
-summed over ranks) / time.
+Metric (BASELINE.json): device-resident encode+decode GB/s of input bytes
+(original_count * buffer_bytes per object, the reference's own formula,
+tests/benchmark.cpp:521-524).
 
-Workload (configs[1]): 128 originals + 128 recovery pieces of 65536 bytes,
-GF(2^8).  Every rank owns its own 64 KiB-per-piece column shard of a larger
-object (64-byte column blocks never interact, so no collective is needed);
-per-GPU work is fixed as N grows -> "scaling": "weak".  To defeat the 256 MiB
-Infinity Cache the step walks over >= 16 distinct buffer sets (> 2x MALL).
+Headline workload (configs[1]): 128 originals + 128 recovery pieces of 65536
+bytes, GF(2^8).  One *step* = one pass over a batch of OBJECTS independent
+objects (default 16, a storage node's stripes): each is encoded and then
+decoded with every original lost (the benchmark's worst case, rebuilt from the
+128 recovery pieces), all through the drop-in C ABI with device pointers in
+async mode; object o of a step runs on HIP stream o % S (S objects in flight,
+--streams).  The batch cycles through >= 16 distinct buffer sets (> 2x the
+256 MiB Infinity Cache), so every step reads HBM.  Every rank codes its own
+objects (64-byte column blocks and objects never interact; no collective):
+"scaling": "weak", value = input bytes of all ranks / max-over-ranks time.
 
-Roofline: the dominant kernel is timed alone with HIP events on the stream it
-runs on (back-to-back calls queued behind a spin kernel); achieved =
-algorithmic bytes per launch ((K_surv + lost) * B for decode, (K + R) * B for
-encode) / mean launch duration, against the 8 TB/s HBM3E peak.
-traffic = HBM bytes per launch from the committed rocprofv3 PMC pass
+configs[4] (`sharded_object`): ONE 32768+32768 x 64 KiB object (2 GiB of
+originals, GF(2^16)) column-sharded over the N ranks -- rank g runs
+leo_amd_encode_slice / leo_amd_decode_slice on its B/N columns of every piece
+-- timed with a barrier and max over ranks ("strong" scaling: the object is
+fixed as N grows).  With N > 1, rank 0 also times the whole object alone on
+its GPU in the same run, so the line carries the 1-GPU time of that object.
+
+Roofline: the dominant kernel of the headline is timed alone with HIP events
+on the stream it runs on (back-to-back calls queued behind a spin kernel);
+achieved = algorithmic bytes per launch ((K + R) * B encode, (K_surv + lost) *
+B decode) / mean launch duration, against the 8 TB/s HBM3E
+peak.  traffic = HBM bytes per launch from the committed rocprofv3 PMC pass
 (tools/pmc_traffic.py), when present for this workload.
 
 cpu_baseline: the reference library compiled from its sources
-(oracle/_ref/libleopard_ref.so, AVX2, single thread -- FF8 has no OpenMP) timed
-on this host on a bounded sample of the same workload; falls back to our
-scalar oracle port if the reference build is absent.
+(oracle/_ref/libleopard_ref.so, AVX2 + OpenMP) on this host: the headline
+workload on 1 core (its FF8 path has no OpenMP), plus the GF(2^16) shapes at 1
+and all allowed threads, warm and cold single-call (the reference's own
+methodology, tests/benchmark.cpp:420-429, 471-480), and the CPU model.
+Falls back to our scalar oracle port if the reference build is absent.
 """
 from __future__ import annotations
 
@@ -42,24 +50,42 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+VP = ctypes.c_void_p
+
+# Benchmarks.md:8-27 (reference, "few year old laptop", AVX2, B = 2560 except 128+128 at 64000),
+# input MB/s (encode, decode): the breadth shapes
+BREADTH = [  # (K, R, B, losses, ref enc MB/s, ref dec MB/s)
+    (100, 10, 2560, 10, 5333.33, 1695.36),
+    (100, 20, 2560, 20, 3878.79, 833.876),
+    (128, 128, 64000, 128, 1964.98, 600.542),
+    (1000, 200, 2560, 200, 1942.34, 367.109),
+    (1000, 1000, 2560, 1000, 1038.54, 365.876),
+    (32768, 32768, 2560, 32768, 471.209, 164.957),
+    (32768, 2048, 2560, 2048, 1359.71, 169.359),
+]
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=1000)
-    ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--K", type=int, default=128)
     ap.add_argument("--R", type=int, default=128)
     ap.add_argument("--bytes", type=int, default=65536)
+    ap.add_argument("--objects", type=int, default=16, help="independent objects per step")
     ap.add_argument("--sets", type=int, default=0, help="buffer sets rotated (0 = enough for >512 MiB)")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--no-secondary", action="store_true",
-                    help="skip the GF(2^16) configs (32768+32768 and 1000+200 x 64 KiB)")
-    ap.add_argument("--no-host", action="store_true", help="skip the host-memory (PCIe-inclusive) rate")
     ap.add_argument("--streams", type=int, default=3,
-                    help="objects in flight: step s runs on HIP stream s %% S (1 = strictly serial steps)")
+                    help="per-call mode: object o of a step runs on HIP stream o %% S")
+    ap.add_argument("--mode", choices=("batch", "calls"), default="batch",
+                    help="batch: a step is one leo_amd_encode_batch + one leo_amd_decode_batch over its objects "
+                         "(one launch each); calls: one leo_encode + leo_decode per object, S streams in flight")
+    ap.add_argument("--sharded-steps", type=int, default=0, help="steps of the configs[4] object (0 = min(steps, 10))")
+    ap.add_argument("--no-sharded", action="store_true", help="skip the configs[4] sharded object")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=5.0)
+    ap.add_argument("--no-secondary", action="store_true", help="skip 1000+200, B=64000 and the breadth shapes")
+    ap.add_argument("--no-host", action="store_true", help="skip the host-memory (PCIe-inclusive) rate")
     return ap.parse_args()
 
 
@@ -83,6 +109,12 @@ def hash_fill_cuda(torch, seed, pieces, nbytes, device):
     return out
 
 
+def ptrs(t, rows=None, lost=()):
+    n = t.shape[0] if rows is None else rows
+    lost = set(lost)
+    return (VP * n)(*[None if i in lost else t[i].data_ptr() for i in range(n)])
+
+
 class Sets:
     """Pre-built pointer arrays (ctypes) for rotating buffer sets."""
 
@@ -90,8 +122,7 @@ class Sets:
         self.k, self.r, self.nbytes = k, r, nbytes
         self.enc_wc = leo.leo_encode_work_count(k, r)
         self.dec_wc = leo.leo_decode_work_count(k, r)
-        VP = ctypes.c_void_p
-        self.orig, self.rec, self.enc_work, self.dec_work = [], [], [], []
+        self.orig, self.enc_work, self.dec_work = [], [], []
         self.p_orig, self.p_encw, self.p_null, self.p_rec, self.p_decw = [], [], [], [], []
         for s in range(nsets):
             o = hash_fill_cuda(torch, 7 + s, k, nbytes, device)
@@ -100,11 +131,11 @@ class Sets:
             self.orig.append(o)
             self.enc_work.append(ew)
             self.dec_work.append(dw)
-            self.p_orig.append((VP * k)(*[o[i].data_ptr() for i in range(k)]))
-            self.p_encw.append((VP * self.enc_wc)(*[ew[i].data_ptr() for i in range(self.enc_wc)]))
+            self.p_orig.append(ptrs(o))
+            self.p_encw.append(ptrs(ew))
             self.p_null.append((VP * k)())  # every original lost
-            self.p_rec.append((VP * r)(*[ew[i].data_ptr() for i in range(r)]))
-            self.p_decw.append((VP * self.dec_wc)(*[dw[i].data_ptr() for i in range(self.dec_wc)]))
+            self.p_rec.append(ptrs(ew, r))
+            self.p_decw.append(ptrs(dw))
         self.n = nsets
 
 
@@ -127,14 +158,89 @@ def main():
     import leopard_amd as leo
     from leopard_amd.sharding import max_over_ranks
     assert leo.leo_init() == 0, leo.last_error()
-    lib = leo.lib
     stream = torch.cuda.current_stream(device)
     leo.set_stream(stream.cuda_stream)
     leo.set_async(True)
 
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    head = headline(args, leo, torch, device, barrier, world, max_over_ranks)
+
+    sharded = None
+    if not args.no_sharded:
+        sharded = configs4_sharded(args, leo, torch, device, barrier, rank, world, max_over_ranks)
+
+    secondary = breadth = host = cpu = None
+    if rank == 0 and not args.no_secondary:
+        secondary = [run_shape(leo, torch, device, *c) for c in
+                     ((1000, 200, 65536, 200), (1000, 200, 64000, 200), (128, 128, 64000, 128))]
+        breadth = [dict(run_shape(leo, torch, device, k, r, b, loss, n=5),
+                        reference_MBps={"encode": re, "decode": rd, "source": "Benchmarks.md:8-27"})
+                   for k, r, b, loss, re, rd in BREADTH]
+    if rank == 0 and not args.no_host:
+        host = host_e2e(leo, args.K, args.R, args.bytes)
+    if rank == 0 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.K, args.R, args.bytes, args.cpu_seconds)
+
+    if rank == 0:
+        k, r, nbytes = args.K, args.R, args.bytes
+        traffic = pmc_traffic(head["dominant"][0], k, r, nbytes)
+        kind, algo, t_kernel = head["dominant"]
+        achieved = algo / t_kernel / 1e9
+        out = {
+            "metric": "device-resident encode+decode GB/s (input bytes/s) at 128+128 and 32768+32768 pieces",
+            "value": head["value"],
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": head["ms_per_step"],
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (counter-hash bytes on device)",
+            "config": {"workload": f"configs[1]: {k}+{r} x {nbytes} B pieces, GF(2^8); step = {args.objects} objects "
+                                   f"per rank, each encoded then decoded with all {k} originals lost, "
+                                   + ("one batched encode + decode launch per step"
+                                      if args.mode == "batch" else f"{head['streams']} objects in flight")
+                                   + f"; {head['sets']} rotating buffer sets"
+                                   + (f"; plus configs[4] (sharded_object): one 32768+32768 x 65536 B object "
+                                      f"column-sharded over {world} GPUs" if sharded else ""),
+                       "original_count": k, "recovery_count": r, "buffer_bytes": nbytes, "losses": k,
+                       "objects_per_step": args.objects, "mode": args.mode,
+                       "field": "FF8" if leo.leo_decode_work_count(k, r) <= 256 else "FF16",
+                       "sharding": "objects per rank (headline); 64-byte column blocks per rank (sharded_object); "
+                                   "no collective"},
+            "modes": head["modes"],
+            "encode_GBps": round(k * nbytes / head["t_enc"] / 1e9, 3),
+            "decode_GBps": round(k * nbytes / head["t_dec"] / 1e9, 3),
+            "encode_us": round(head["t_enc"] * 1e6, 3),
+            "decode_us": round(head["t_dec"] * 1e6, 3),
+            "roofline": {"bound": "hbm", "kernel": kind, "achieved": round(achieved, 2),
+                         "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                         "traffic": traffic.get("bytes"), "traffic_source": traffic.get("source"),
+                         "algorithmic_bytes_per_launch": algo},
+            "cpu_baseline": cpu,
+            "sharded_object": sharded,
+            "host_e2e": host,
+            "secondary": secondary,
+            "breadth": breadth,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def headline(args, leo, torch, device, barrier, world, max_over_ranks):
+    lib = leo.lib
+    stream = torch.cuda.current_stream(device)
     k, r, nbytes = args.K, args.R, args.bytes
     per_set = (k + leo.leo_encode_work_count(k, r) + leo.leo_decode_work_count(k, r)) * nbytes
-    nsets = args.sets or max(16, -(-(512 << 20) // per_set))
+    nsets = args.sets or max(16, args.objects, -(-(512 << 20) // per_set))
     sets = Sets(leo, torch, k, r, nbytes, nsets, device)
     torch.cuda.synchronize()
 
@@ -152,31 +258,46 @@ def main():
         assert enc(i) == 0
     torch.cuda.synchronize()
 
-    def barrier():
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
+    # Per-call mode: object o of a step (encode of buffer set i, then the
+    # decode of its recovery pieces) runs on stream o % S; calls on one stream
+    # stay ordered and concurrent objects never share buffers.
+    nstreams = max(1, args.streams)
+    streams = [torch.cuda.Stream(device) for _ in range(nstreams)]
 
-    # Objects in flight: step s (encode of buffer set i, then the decode of its
-    # recovery pieces) runs on stream s % S, so up to S independent objects are
-    # coded concurrently -- how a storage node keeps the GPU busy with stripes
-    # whose single calls are too small to fill 256 CUs.  Steps on one stream
-    # stay ordered; buffer sets rotate over >= 16 sets, so concurrent steps
-    # never share buffers.
-    streams = [torch.cuda.Stream(device) for _ in range(max(1, args.streams))]
-
-    def run_steps(nsteps, nstreams):
+    def run_calls(nsteps, ns):
         for s in range(nsteps):
-            i = s % sets.n
-            leo.set_stream(streams[s % nstreams].cuda_stream)
-            if enc(i) != 0 or dec(i) != 0:
+            for o in range(args.objects):
+                i = (s * args.objects + o) % sets.n
+                leo.set_stream(streams[o % ns].cuda_stream)
+                if enc(i) != 0 or dec(i) != 0:
+                    raise RuntimeError(leo.last_error())
+
+    # Batch mode: step s covers buffer sets (s * objects + o) % n, o < objects:
+    # one leo_amd_encode_batch and one leo_amd_decode_batch (one kernel launch
+    # each) on one stream; the pointer arrays are built once per distinct batch.
+    PP = ctypes.POINTER(VP)
+    nbatches = sets.n // max(1, args.objects) if sets.n % max(1, args.objects) == 0 else sets.n
+    batches = []
+    for bi in range(nbatches):
+        ids = [(bi * args.objects + o) % sets.n for o in range(args.objects)]
+        mk = lambda arrs: (PP * len(arrs))(*[ctypes.cast(a, PP) for a in arrs])  # noqa: E731
+        batches.append((mk([sets.p_orig[i] for i in ids]), mk([sets.p_encw[i] for i in ids]),
+                        mk([sets.p_null[i] for i in ids]), mk([sets.p_rec[i] for i in ids]),
+                        mk([sets.p_decw[i] for i in ids])))
+
+    def run_batches(nsteps, _ns):
+        leo.set_stream(stream.cuda_stream)
+        for s in range(nsteps):
+            bo, bw, bn, br, bd = batches[s % nbatches]
+            if (lib.leo_amd_encode_batch(args.objects, nbytes, k, r, sets.enc_wc, bo, bw) != 0 or
+                    lib.leo_amd_decode_batch(args.objects, nbytes, k, r, sets.dec_wc, bn, br, bd) != 0):
                 raise RuntimeError(leo.last_error())
 
-    def timed(nstreams):
-        run_steps(args.warmup, nstreams)
+    def timed(run, ns):
+        run(args.warmup, ns)
         barrier()
         t0 = time.perf_counter()
-        run_steps(args.steps, nstreams)
+        run(args.steps, ns)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         el = max_over_ranks(t1 - t0)
@@ -184,8 +305,18 @@ def main():
             barrier()
         return el
 
-    elapsed = timed(len(streams))
-    elapsed_serial = timed(1) if len(streams) > 1 else elapsed
+    # correctness gate of the batch path before timing it
+    for i in range(sets.n):
+        sets.dec_work[i].zero_()
+    run_batches(1, 1)
+    torch.cuda.synchronize()
+    for o in range(args.objects):
+        i = o % sets.n
+        assert torch.equal(sets.dec_work[i][:k], sets.orig[i]), "batch decode mismatch"
+    elapsed_calls = timed(run_calls, nstreams)
+    elapsed_serial = timed(run_calls, 1)
+    elapsed_batch = timed(run_batches, 1)
+    elapsed = elapsed_batch if args.mode == "batch" else elapsed_calls
     leo.set_stream(stream.cuda_stream)
 
     # Per-launch kernel duration with HIP events on the launch stream: a spin
@@ -208,108 +339,136 @@ def main():
 
     t_enc = time_calls(enc)
     t_dec = time_calls(dec)
-    in_bytes = k * nbytes
     algo_enc = (k + r) * nbytes
     algo_dec = (r + k) * nbytes  # R surviving pieces read + K lost originals written (full loss)
     dominant = ("decode", algo_dec, t_dec) if t_dec >= t_enc else ("encode", algo_enc, t_enc)
+    in_step = k * nbytes * args.objects
 
-    secondary = None
-    if not args.no_secondary and rank == 0:
-        secondary = [run_secondary(leo, torch, device, kk, rr, ll) for kk, rr, ll in
-                     ((32768, 32768, 32768), (1000, 200, 200))]
-    host = host_e2e(leo, k, r, nbytes) if rank == 0 and not args.no_host else None
+    def rate(el, note):
+        return {"value": round(world * in_step * args.steps / el / 1e9, 3),
+                "ms_per_step": round(el / args.steps * 1e3, 4), "note": note}
 
-    cpu = None
-    if rank == 0 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(k, r, nbytes, args.cpu_seconds)
-
-    traffic = pmc_traffic(dominant[0], k, r, nbytes)
-    if rank == 0:
-        value = world * in_bytes * args.steps / elapsed / 1e9
-        achieved = dominant[1] / dominant[2] / 1e9
-        out = {
-            "metric": "device-resident encode+decode GB/s (input bytes/s) at 128+128 and 32768+32768 pieces",
-            "value": round(value, 3),
-            "unit": "GB/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u8",
-            "data": "synthetic (counter-hash bytes on device)",
-            "config": {"workload": f"{k}+{r} x {nbytes} B pieces, GF(2^8), encode + full-loss decode per step, "
-                                   f"device-resident, {sets.n} rotating buffer sets, "
-                                   f"{len(streams)} objects in flight",
-                       "original_count": k, "recovery_count": r, "buffer_bytes": nbytes, "losses": k,
-                       "field": "FF8" if leo.leo_decode_work_count(k, r) <= 256 else "FF16",
-                       "objects_in_flight": len(streams),
-                       "sharding": "64-byte column blocks per rank, no collective"},
-            "serial": {"value": round(world * in_bytes * args.steps / elapsed_serial / 1e9, 3),
-                       "ms_per_step": round(elapsed_serial / args.steps * 1e3, 4),
-                       "note": "same steps, one stream (each step waits for the previous)"},
-            "encode_GBps": round(in_bytes / t_enc / 1e9, 3),
-            "decode_GBps": round(in_bytes / t_dec / 1e9, 3),
-            "encode_us": round(t_enc * 1e6, 3),
-            "decode_us": round(t_dec * 1e6, 3),
-            "roofline": {"bound": "hbm", "kernel": dominant[0], "achieved": round(achieved, 2),
-                         "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                         "traffic": traffic.get("bytes"), "traffic_source": traffic.get("source"),
-                         "algorithmic_bytes_per_launch": dominant[1]},
-            "cpu_baseline": cpu,
-            "host_e2e": host,
-        }
-        if secondary:
-            out["secondary"] = secondary
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    res = {"value": round(world * in_step * args.steps / elapsed / 1e9, 3),
+           "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+           "modes": {
+               "batch": rate(elapsed_batch, "leo_amd_encode_batch + leo_amd_decode_batch over the step's objects, "
+                                            "one launch each, one stream"),
+               "calls_in_flight": rate(elapsed_calls, f"one leo_encode + leo_decode per object, {nstreams} objects "
+                                                      f"in flight on {nstreams} streams"),
+               "serial": rate(elapsed_serial, "one leo_encode + leo_decode per object on one stream: each call "
+                                              "waits for the previous (a plain drop-in caller)")},
+           "t_enc": t_enc, "t_dec": t_dec, "dominant": dominant, "sets": sets.n, "streams": nstreams}
+    del sets
+    torch.cuda.empty_cache()
+    return res
 
 
-def run_secondary(leo, torch, device, k, r, loss):
-    """GF(2^16) configs of BASELINE.json (configs[3], configs[2]) at 64 KiB:
-    encode, then decode with `loss` originals lost (the benchmark's
-    ShuffleDeck16 pattern, tests/benchmark.cpp:440-467) -- a few calls each."""
-    sys.path.insert(0, os.path.join(REPO, "tests"))
-    import oracle_lib as ol
-    nbytes = 65536
+def configs4_sharded(args, leo, torch, device, barrier, rank, world, max_over_ranks):
+    """BASELINE configs[4]: one 32768+32768 x 64 KiB object, column-sharded over
+    the ranks (leopard_amd.sharding -> leo_amd_encode_slice / decode_slice; the
+    codec being sharded is LeopardFF16.cpp:1397-1467, 1652-1775).  Each rank
+    holds every piece at full size and touches only its columns."""
+    from leopard_amd.sharding import shard_for_rank
     lib = leo.lib
-    VP = ctypes.c_void_p
+    k = r = 32768
+    b = 65536
+    wc, dwc = leo.leo_encode_work_count(k, r), leo.leo_decode_work_count(k, r)
+    data = hash_fill_cuda(torch, 7, k, b, device)
+    work = torch.empty((wc, b), dtype=torch.uint8, device=device)
+    dwork = torch.empty((dwc, b), dtype=torch.uint8, device=device)
+    po, pw, pr, pd = ptrs(data), ptrs(work), ptrs(work, r), ptrs(dwork)
+    pn = (VP * k)()  # every original lost
+    stream = torch.cuda.current_stream(device)
+    leo.set_stream(stream.cuda_stream)
+
+    def step(off, size):
+        if lib.leo_amd_encode_slice(b, off, size, k, r, wc, po, pw) != 0:
+            raise RuntimeError(leo.last_error())
+        if lib.leo_amd_decode_slice(b, off, size, k, r, dwc, pn, pr, pd) != 0:
+            raise RuntimeError(leo.last_error())
+
+    off, size = shard_for_rank(b, rank, world)
+    step(off, size)
+    torch.cuda.synchronize()
+    ok = bool(torch.equal(dwork[:k, off:off + size], data[:, off:off + size]))
+    nsteps = args.sharded_steps or max(1, min(args.steps, 10))
+    step(off, size)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(nsteps):
+        step(off, size)
+    torch.cuda.synchronize()
+    el = max_over_ranks(time.perf_counter() - t0)
+    n1_ms = None
+    if world > 1:  # the same object on one GPU (rank 0 alone) for the strong-scaling ratio
+        barrier()
+        if rank == 0:
+            step(0, b)
+            torch.cuda.synchronize()
+            a = time.perf_counter()
+            for _ in range(max(1, nsteps // 2)):
+                step(0, b)
+            torch.cuda.synchronize()
+            n1_ms = (time.perf_counter() - a) / max(1, nsteps // 2) * 1e3
+        barrier()
+    ms = el / nsteps * 1e3
+    algo = 2 * (k + r) * b  # encode (K + R) * B + full-loss decode (R + K) * B, whole object
+    res = {"workload": f"configs[4]: one {k}+{r} x {b} B object (GF(2^16), encode + full-loss decode), "
+                       f"column-sharded over {world} GPU(s): {b // world if b % world == 0 else size} B of every "
+                       f"piece per rank via leo_amd_encode_slice / leo_amd_decode_slice",
+           "value": round(k * b * nsteps / el / 1e9, 3), "unit": "GB/s", "scaling": "strong",
+           "n_gpus": world, "ms_per_step": round(ms, 3), "steps": nsteps, "roundtrip_ok": ok,
+           "roofline": {"bound": "hbm", "achieved_per_gpu": round(algo / world / (ms / 1e3) / 1e9, 2),
+                        "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                        "frac": round(algo / world / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
+                        "algorithmic_bytes_per_step": algo}}
+    if n1_ms is not None:
+        res["one_gpu_ms_per_step"] = round(n1_ms, 3)
+        res["speedup_vs_one_gpu"] = round(n1_ms / ms, 3)
+    del data, work, dwork
+    torch.cuda.empty_cache()
+    return res
+
+
+def run_shape(leo, torch, device, k, r, nbytes, loss, n=3):
+    """One (K, R, B) shape: encode, then decode with `loss` originals lost (the
+    benchmark's ShuffleDeck16 pattern, tests/benchmark.cpp:440-467) -- a few
+    back-to-back calls each, timed with HIP events on the call stream."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_lib as ol  # the reference benchmark's PCG + ShuffleDeck16 loss pattern
+    lib = leo.lib
     o = hash_fill_cuda(torch, 7, k, nbytes, device)
     ew = torch.empty((leo.leo_encode_work_count(k, r), nbytes), dtype=torch.uint8, device=device)
     dw = torch.empty((leo.leo_decode_work_count(k, r), nbytes), dtype=torch.uint8, device=device)
     lo, lr = ol.benchmark_losses(k, r, loss, seed=2, trial=0)
-    los, lrs = set(lo), set(lr)
-    po = (VP * k)(*[o[i].data_ptr() for i in range(k)])
-    pe = (VP * ew.shape[0])(*[ew[i].data_ptr() for i in range(ew.shape[0])])
-    pn = (VP * k)(*[None if i in los else o[i].data_ptr() for i in range(k)])
-    pr = (VP * r)(*[None if i in lrs else ew[i].data_ptr() for i in range(r)])
-    pd = (VP * dw.shape[0])(*[dw[i].data_ptr() for i in range(dw.shape[0])])
+    po, pe, pd = ptrs(o), ptrs(ew), ptrs(dw)
+    pn, pr = ptrs(o, lost=lo), ptrs(ew, r, lost=lr)
     s = torch.cuda.current_stream(device)
     leo.set_stream(s.cuda_stream)
 
-    def t(fn, n=3):
+    def t(fn):
         assert fn() == 0, leo.last_error()
         s.synchronize()
         a = torch.cuda.Event(enable_timing=True)
-        b = torch.cuda.Event(enable_timing=True)
+        z = torch.cuda.Event(enable_timing=True)
         a.record(s)
         for _ in range(n):
             assert fn() == 0, leo.last_error()
-        b.record(s)
-        b.synchronize()
-        return a.elapsed_time(b) / 1e3 / n
+        z.record(s)
+        z.synchronize()
+        return a.elapsed_time(z) / 1e3 / n
 
     te = t(lambda: lib.leo_encode(nbytes, k, r, ew.shape[0], po, pe))
     td = t(lambda: lib.leo_decode(nbytes, k, r, dw.shape[0], pn, pr, pd))
     idx = torch.tensor(lo, device=device)
     ok = bool(torch.equal(dw.index_select(0, idx), o.index_select(0, idx)))
     inb = k * nbytes
-    res = {"workload": f"{k}+{r} x {nbytes} B, GF(2^16), {loss} originals lost", "encode_GBps": round(inb / te / 1e9, 3),
+    field = "GF(2^8)" if leo.leo_decode_work_count(k, r) <= 256 else "GF(2^16)"
+    res = {"workload": f"{k}+{r} x {nbytes} B, {field}, {loss} originals lost", "encode_GBps": round(inb / te / 1e9, 3),
            "decode_GBps": round(inb / td / 1e9, 3), "encode_decode_GBps": round(inb / (te + td) / 1e9, 3),
-           "encode_ms": round(te * 1e3, 3), "decode_ms": round(td * 1e3, 3), "roundtrip_ok": ok}
+           "encode_us": round(te * 1e6, 2), "decode_us": round(td * 1e6, 2), "roundtrip_ok": ok,
+           "roofline_frac": {"encode": round((k + r) * nbytes / te / 1e9 / HBM_PEAK_GBPS, 4),
+                             "decode": round((r + k) * nbytes / td / 1e9 / HBM_PEAK_GBPS, 4)}}
     del o, ew, dw
     torch.cuda.empty_cache()
     return res
@@ -367,18 +526,92 @@ def pmc_traffic(kernel, k, r, nbytes):
     return {}
 
 
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(k, r, nbytes, seconds):
-    """Reference AVX2 library (or our scalar port) on the host, 1 thread."""
+    """The reference library (or our scalar port) on this host.
+
+    value: the headline workload (128+128 x 64 KiB, encode + full-loss decode)
+    on 1 core, warm buffers (the reference's GF(2^8) path is single-threaded).
+    detail: cold single calls as tests/benchmark.cpp:420-429, 471-480 time them
+    (fresh zero-filled buffers, first touch inside the call, one call), and the
+    GF(2^16) shapes (1000+200 x 64 KiB; 32768+32768 on a bounded 8 KiB-per-piece
+    sample) at 1 thread and at every allowed thread (OpenMP)."""
     import numpy as np
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_lib as ol
-    os.environ.setdefault("OMP_NUM_THREADS", "1")
     codec, kind = ol.reference(), "reference"
     if codec is None:
         codec, kind = ol.oracle(), "port"
+    try:
+        gomp = ctypes.CDLL("libgomp.so.1")
+    except OSError:
+        gomp = None
+    allowed = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    threads = max(1, min(allowed, int(os.environ.get("OMP_NUM_THREADS", allowed) or allowed)))
+
+    def set_threads(n):
+        if gomp is not None:
+            gomp.omp_set_num_threads(int(n))
+
+    cache = {}
+
+    def shape(kk, rr, bb, loss, reps, cold):
+        if (kk, bb) not in cache:
+            cache[(kk, bb)] = ol.hash_bytes(7, kk, bb)
+        data = cache[(kk, bb)]
+        codec.encode(ol.hash_bytes(1, 300, 64), 37)  # OpenMP pool up, as after the reference's leo_init
+        wce, wcd = codec.encode_work_count(kk, rr), codec.decode_work_count(kk, rr)
+        lo, lr = ol.benchmark_losses(kk, rr, loss, seed=2, trial=0)
+        los, lrs = set(lo), set(lr)
+        res = {}
+        if cold:  # fresh zero pages, one call each (the reference benchmark's methodology)
+            work = np.zeros((wce, bb), dtype=np.uint8)
+            a = time.perf_counter()
+            codec.encode_raw(bb, kk, rr, wce, [data[i].ctypes.data for i in range(kk)],
+                             [work[i].ctypes.data for i in range(wce)])
+            te = time.perf_counter() - a
+            dwork = np.zeros((wcd, bb), dtype=np.uint8)
+            a = time.perf_counter()
+            codec.decode_raw(bb, kk, rr, wcd, [None if i in los else data[i].ctypes.data for i in range(kk)],
+                             [None if i in lrs else work[i].ctypes.data for i in range(rr)],
+                             [dwork[i].ctypes.data for i in range(wcd)])
+            td = time.perf_counter() - a
+            res["cold_GBps"] = {"encode": round(kk * bb / te / 1e9, 3), "decode": round(kk * bb / td / 1e9, 3)}
+        work = np.zeros((wce, bb), dtype=np.uint8)
+        dwork = np.zeros((wcd, bb), dtype=np.uint8)
+        pe = [work[i].ctypes.data for i in range(wce)]
+        po = [data[i].ctypes.data for i in range(kk)]
+        pn = [None if i in los else data[i].ctypes.data for i in range(kk)]
+        pr = [None if i in lrs else work[i].ctypes.data for i in range(rr)]
+        pd = [dwork[i].ctypes.data for i in range(wcd)]
+        codec.encode_raw(bb, kk, rr, wce, po, pe)
+        codec.decode_raw(bb, kk, rr, wcd, pn, pr, pd)
+        be = bd = float("inf")
+        for _ in range(reps):
+            a = time.perf_counter()
+            codec.encode_raw(bb, kk, rr, wce, po, pe)
+            b = time.perf_counter()
+            codec.decode_raw(bb, kk, rr, wcd, pn, pr, pd)
+            c = time.perf_counter()
+            be, bd = min(be, b - a), min(bd, c - b)
+        assert all(np.array_equal(dwork[i], data[i]) for i in lo)
+        res["warm_GBps"] = {"encode": round(kk * bb / be / 1e9, 3), "decode": round(kk * bb / bd / 1e9, 3)}
+        return res
+
+    # headline: warm loop for `seconds` on 1 core
+    set_threads(1)
     data = ol.hash_bytes(7, k, nbytes)
-    wc_e = codec.encode_work_count(k, r)
-    wc_d = codec.decode_work_count(k, r)
+    wc_e, wc_d = codec.encode_work_count(k, r), codec.decode_work_count(k, r)
     work = np.zeros((wc_e, nbytes), dtype=np.uint8)
     dwork = np.zeros((wc_d, nbytes), dtype=np.uint8)
     po = [data[i].ctypes.data for i in range(k)]
@@ -386,7 +619,6 @@ def cpu_baseline(k, r, nbytes, seconds):
     pn = [None] * k
     pr = [work[i].ctypes.data for i in range(r)]
     pd = [dwork[i].ctypes.data for i in range(wc_d)]
-    # warm (first touch)
     assert codec.encode_raw(nbytes, k, r, wc_e, po, pe) == 0
     assert codec.decode_raw(nbytes, k, r, wc_d, pn, pr, pd) == 0
     t_enc = t_dec = 0.0
@@ -403,10 +635,18 @@ def cpu_baseline(k, r, nbytes, seconds):
         steps += 1
     assert np.array_equal(dwork[:k], data)
     inb = k * nbytes
+    detail = {"cpu_model": cpu_model(), "threads_allowed": threads,
+              f"{k}+{r}x{nbytes}_1thread": shape(k, r, nbytes, k, 3, True)}
+    for th in sorted({1, threads}):
+        set_threads(th)
+        detail[f"1000+200x65536_{th}threads"] = shape(1000, 200, 65536, 200, 3, True)
+        detail[f"32768+32768x8192_{th}threads"] = shape(32768, 32768, 8192, 32768, 1, th == threads)
+    set_threads(threads)
     return {"value": round(inb * steps / (t_enc + t_dec) / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": kind,
             "sample": f"{steps} encode+decode steps of {k}+{r} x {nbytes} B (full loss), warm buffers, "
-                      f"{t_enc + t_dec:.1f} s; encode {inb * steps / t_enc / 1e9:.3f} GB/s, "
-                      f"decode {inb * steps / t_dec / 1e9:.3f} GB/s"}
+                      f"{t_enc + t_dec:.1f} s on 1 core of {cpu_model()}; encode {inb * steps / t_enc / 1e9:.3f} "
+                      f"GB/s, decode {inb * steps / t_dec / 1e9:.3f} GB/s",
+            "detail": detail}
 
 
 if __name__ == "__main__":

@@ -44,6 +44,24 @@ LEO_EXPORT LeopardResult leo_amd_decode_slice(
     const void* const* const original_data, const void* const* const recovery_data,
     void** work_data);
 
+/* Batches: object_count independent objects of one shape (same buffer_bytes,
+ * counts and work_count), each with exactly the semantics of one leo_encode /
+ * leo_decode call; original_data[o], recovery_data[o], work_data[o] are object
+ * o's pointer arrays.  Every object is validated first: the first failing
+ * object's result is returned and nothing runs.  Device-resident GF(2^8)
+ * objects (n <= 256) on one device are coded by ONE kernel launch over every
+ * object's columns -- a single 64 KiB-piece object gives each CU one
+ * workgroup, a batch fills the GPU; other batches run object by object.
+ * Decoding objects may have different erasure patterns. */
+LEO_EXPORT LeopardResult leo_amd_encode_batch(
+    unsigned object_count, uint64_t buffer_bytes, unsigned original_count, unsigned recovery_count,
+    unsigned work_count, const void* const* const* original_data, void** const* work_data);
+
+LEO_EXPORT LeopardResult leo_amd_decode_batch(
+    unsigned object_count, uint64_t buffer_bytes, unsigned original_count, unsigned recovery_count,
+    unsigned work_count, const void* const* const* original_data, const void* const* const* recovery_data,
+    void** const* work_data);
+
 /* Number of HIP devices usable by the library (0 when none / not gfx950). */
 LEO_EXPORT int leo_amd_device_count(void);
 

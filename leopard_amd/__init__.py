@@ -33,7 +33,8 @@ LEO_VERSION = 2
 
 __all__ = [
     "LEO_VERSION", "LeopardResult", "leo_init", "leo_result_string", "leo_encode_work_count", "leo_encode",
-    "leo_decode_work_count", "leo_decode", "leo_amd_encode_slice", "leo_amd_decode_slice", "set_stream",
+    "leo_decode_work_count", "leo_decode", "leo_amd_encode_slice", "leo_amd_decode_slice", "leo_amd_encode_batch",
+    "leo_amd_decode_batch", "set_stream",
     "set_async", "set_device", "device_count", "table", "last_error", "encode", "decode", "LIB_PATH", "lib",
 ]
 
@@ -69,6 +70,8 @@ def _load():
         "leo_decode": (i, [u64, u, u, u, pp, pp, pp]),
         "leo_amd_encode_slice": (i, [u64, u64, u64, u, u, u, pp, pp]),
         "leo_amd_decode_slice": (i, [u64, u64, u64, u, u, u, pp, pp, pp]),
+        "leo_amd_encode_batch": (i, [u, u64, u, u, u, ctypes.POINTER(pp), ctypes.POINTER(pp)]),
+        "leo_amd_decode_batch": (i, [u, u64, u, u, u, ctypes.POINTER(pp), ctypes.POINTER(pp), ctypes.POINTER(pp)]),
         "leo_amd_set_stream": (None, [vp]),
         "leo_amd_set_async": (None, [i]),
         "leo_amd_set_device": (None, [i]),
@@ -135,6 +138,29 @@ def leo_amd_decode_slice(buffer_bytes, byte_offset, slice_bytes, original_count,
     return LeopardResult(lib.leo_amd_decode_slice(buffer_bytes, byte_offset, slice_bytes, original_count,
                                                   recovery_count, work_count, _ptrs(original_data),
                                                   _ptrs(recovery_data), _ptrs(work_data)))
+
+
+def _ptr_arrays(seqs):
+    """List of pointer sequences -> (void**)[count] (keeps the arrays alive in .keep)."""
+    arrs = [_ptrs(q) for q in seqs]
+    outer = (ctypes.POINTER(ctypes.c_void_p) * max(len(arrs), 1))(
+        *[ctypes.cast(a, ctypes.POINTER(ctypes.c_void_p)) for a in arrs])
+    outer.keep = arrs
+    return outer
+
+
+def leo_amd_encode_batch(buffer_bytes, original_count, recovery_count, work_count, original_data,
+                         work_data) -> LeopardResult:
+    """original_data / work_data: one pointer sequence per object (include/leopard_amd.h)."""
+    return LeopardResult(lib.leo_amd_encode_batch(len(original_data), buffer_bytes, original_count, recovery_count,
+                                                  work_count, _ptr_arrays(original_data), _ptr_arrays(work_data)))
+
+
+def leo_amd_decode_batch(buffer_bytes, original_count, recovery_count, work_count, original_data, recovery_data,
+                         work_data) -> LeopardResult:
+    return LeopardResult(lib.leo_amd_decode_batch(len(original_data), buffer_bytes, original_count, recovery_count,
+                                                  work_count, _ptr_arrays(original_data), _ptr_arrays(recovery_data),
+                                                  _ptr_arrays(work_data)))
 
 
 def set_stream(stream_handle: Optional[int]) -> None:

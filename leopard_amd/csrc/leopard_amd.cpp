@@ -115,10 +115,19 @@ struct Workspace {
     hipStream_t stream = nullptr;
     uint8_t* dbuf = nullptr;
     size_t dsize = 0;
-    uint8_t* hstage = nullptr;
-    size_t hsize = 0;
-    hipEvent_t stage_done = nullptr;
-    bool stage_pending = false;
+    // Pinned staging ring for small host->device uploads (pointer tables,
+    // batch argument blocks, decoder state): a slot is rewritten only after
+    // the copy issued from it kBack uploads ago has completed, so back-to-back
+    // async calls do not wait for each other's copies.
+    static constexpr int kStageSlots = 8;
+    struct StageSlot {
+        uint8_t* host = nullptr;
+        size_t size = 0;
+        hipEvent_t done = nullptr;
+        bool pending = false;
+    };
+    StageSlot stage[kStageSlots];
+    unsigned stage_next = 0;
     // Host-memory pipeline ring: two slots of `slot_bytes` in pinned host memory
     // and in device memory, one stream and two events per slot.
     uint8_t* ring_host = nullptr;
@@ -171,20 +180,33 @@ struct Workspace {
         dsize = want;
         return Leopard_Success;
     }
-    // Staging buffer free for writing (previous upload finished).
-    LeopardResult reserve_stage(size_t bytes) {
-        if (stage_pending) {
-            HIP_OK(hipEventSynchronize(stage_done), "wait staging");
-            stage_pending = false;
+    // Copies `bytes` from host memory src (or, with src == nullptr, lets
+    // fill(host) write them) through the next ring slot into device memory dst,
+    // ordered on stream s.
+    template <class Fill>
+    LeopardResult upload(void* dst, size_t bytes, hipStream_t s, Fill&& fill) {
+        StageSlot& sl = stage[stage_next];
+        stage_next = (stage_next + 1) % kStageSlots;
+        if (sl.pending) {
+            HIP_OK(hipEventSynchronize(sl.done), "wait staging slot");
+            sl.pending = false;
         }
-        if (!stage_done) HIP_OK(hipEventCreateWithFlags(&stage_done, hipEventDisableTiming), "event");
-        if (bytes <= hsize) return Leopard_Success;
-        if (hstage) HIP_OK(hipHostFree(hstage), "free staging");
-        hstage = nullptr;
-        size_t want = std::max<size_t>(bytes, std::max<size_t>(hsize * 2, 1 << 16));
-        HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&hstage), want, hipHostMallocDefault), "pinned staging");
-        hsize = want;
+        if (!sl.done) HIP_OK(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming), "event");
+        if (bytes > sl.size) {
+            if (sl.host) HIP_OK(hipHostFree(sl.host), "free staging");
+            sl.host = nullptr;
+            const size_t want = std::max<size_t>(bytes, std::max<size_t>(sl.size * 2, 1 << 16));
+            HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&sl.host), want, hipHostMallocDefault), "pinned staging");
+            sl.size = want;
+        }
+        fill(sl.host);
+        HIP_OK(hipMemcpyAsync(dst, sl.host, bytes, hipMemcpyHostToDevice, s), "upload");
+        HIP_OK(hipEventRecord(sl.done, s), "record staging");
+        sl.pending = true;
         return Leopard_Success;
+    }
+    LeopardResult upload(void* dst, const void* src, size_t bytes, hipStream_t s) {
+        return upload(dst, bytes, s, [&](uint8_t* h) { std::memcpy(h, src, bytes); });
     }
 };
 thread_local std::vector<std::unique_ptr<Workspace>> tws;
@@ -269,15 +291,11 @@ struct MapBuilder {
         pending.push_back({&pm, at});
     }
     size_t bytes() const { return staged.size() * sizeof(uint64_t); }
-    // Copies the tables into pinned staging and enqueues the H2D copy into dev.
+    // Enqueues the upload of the tables into dev (through the staging ring).
     LeopardResult flush(Workspace& ws, uint64_t* dev, hipStream_t s) {
         if (staged.empty()) return Leopard_Success;
-        LeopardResult r = ws.reserve_stage(bytes());
+        LeopardResult r = ws.upload(dev, staged.data(), bytes(), s);
         if (r != Leopard_Success) return r;
-        std::memcpy(ws.hstage, staged.data(), bytes());
-        HIP_OK(hipMemcpyAsync(dev, ws.hstage, bytes(), hipMemcpyHostToDevice, s), "upload piece tables");
-        HIP_OK(hipEventRecord(ws.stage_done, s), "record staging");
-        ws.stage_pending = true;
         for (auto& p : pending) p.map->table = dev + p.index;
         return Leopard_Success;
     }
@@ -327,6 +345,22 @@ LeopardResult finish(const Call& c, bool force_sync) {
 
 // --------------------------------------------------------------- encode ----
 
+// GF(2^8) encoder argument block of one object: columns [off, off + bytes)
+// of every piece (bytes <= kFf8MaxLaunchBytes).
+void fill_enc8(Ff8EncArgs& a, const DeviceTables* t, unsigned K, unsigned R, const void* const* orig, void** work,
+               uint64_t off, uint64_t bytes) {
+    const unsigned m = next_pow2(R);
+    std::memset(&a, 0, sizeof(a));
+    for (unsigned i = 0; i < K; ++i) a.ptr[i] = uint64_t(reinterpret_cast<uintptr_t>(orig[i])) + off;
+    for (unsigned i = 0; i < R; ++i) a.ptr[K + i] = uint64_t(reinterpret_cast<uintptr_t>(work[i])) + off;
+    a.sktab = t->sktab8;
+    a.fused = t->fused8 + size_t(log2u(m) - 1) * 256 * kTab8Dwords;
+    a.K = K;
+    a.R = R;
+    a.nchunks = (K + m - 1) / m;
+    a.nunits = uint32_t(bytes / 4);
+}
+
 // Device-resident encode of pieces [off, off + bytes) (reference:
 // leo_encode -> ff8|ff16::ReedSolomonEncode, leopard.cpp:162-197).
 LeopardResult encode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, unsigned R, const void* const* orig,
@@ -339,17 +373,9 @@ LeopardResult encode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
 
     if (!ff16) {  // n <= 256: one fused kernel, launch data by value (rs_ff8.hip)
         Ff8EncArgs a;
-        std::memset(&a, 0, sizeof(a));
-        a.sktab = c.t->sktab8;
-        a.fused = c.t->fused8 + size_t(Tm - 1) * 256 * kTab8Dwords;
-        a.K = K;
-        a.R = R;
-        a.nchunks = nchunks;
         // one launch per <= 4 GiB of columns (the kernel counts dword columns in 32 bits)
         for (uint64_t pos = 0; pos < bytes; pos += kFf8MaxLaunchBytes) {
-            for (unsigned i = 0; i < K; ++i) a.ptr[i] = uint64_t(reinterpret_cast<uintptr_t>(orig[i])) + off + pos;
-            for (unsigned i = 0; i < R; ++i) a.ptr[K + i] = uint64_t(reinterpret_cast<uintptr_t>(work[i])) + off + pos;
-            a.nunits = uint32_t(std::min(kFf8MaxLaunchBytes, bytes - pos) / 4);
+            fill_enc8(a, c.t, K, R, orig, work, off + pos, std::min(kFf8MaxLaunchBytes, bytes - pos));
             HIP_OK(launch_ff8_encode(Tm, a, c.s), "encode kernel");
         }
         return Leopard_Success;
@@ -439,10 +465,10 @@ LeopardResult xor_device(Call& c, uint64_t bytes, uint64_t off, const void* cons
 // FF8 error locator on the host (n <= 256 positions, a few thousand integer ops):
 // el = FWHT(LogWalsh * FWHT(erasures)) mod 255 (LeopardFF8.cpp:1848-1853).  The
 // last pattern is cached per thread (repeated erasure patterns are common).
-void error_locator8(const std::vector<uint32_t>& erased, uint32_t* el_bytes) {
+void error_locator8(const uint32_t* erased, uint32_t* el_bytes) {
     thread_local uint32_t last_pattern[8] = {~0u, 0, 0, 0, 0, 0, 0, 0};
     thread_local uint32_t last_el[kFf8Ptrs / 4];
-    if (std::memcmp(last_pattern, erased.data(), sizeof(last_pattern)) != 0) {
+    if (std::memcmp(last_pattern, erased, sizeof(last_pattern)) != 0) {
         const GaloisField& f = field8();
         uint16_t e[256];
         for (unsigned p = 0; p < 256; ++p) e[p] = (erased[p >> 5] >> (p & 31)) & 1u;
@@ -452,7 +478,7 @@ void error_locator8(const std::vector<uint32_t>& erased, uint32_t* el_bytes) {
         for (unsigned q = 0; q < 64; ++q)
             last_el[q] = uint32_t(e[4 * q] % 255u) | uint32_t(e[4 * q + 1] % 255u) << 8 |
                          uint32_t(e[4 * q + 2] % 255u) << 16 | uint32_t(e[4 * q + 3] % 255u) << 24;
-        std::memcpy(last_pattern, erased.data(), sizeof(last_pattern));
+        std::memcpy(last_pattern, erased, sizeof(last_pattern));
     }
     std::memcpy(el_bytes, last_el, sizeof(last_el));
 }
@@ -467,24 +493,33 @@ bool ff8_half_decoder_enabled() {
     return v;
 }
 
-LeopardResult decode_device8(Call& c, uint64_t bytes, uint64_t off, unsigned K, unsigned R, unsigned m, unsigned Tn,
-                             const void* const* orig, const void* const* rec, void** work,
-                             const std::vector<uint32_t>& erased) {
-    Ff8DecArgs a;
+// GF(2^8) erasure bitmap over 256 positions: error_locations[] = 1 at lost
+// recoveries, [R, m) and lost originals (LeopardFF8.cpp:1825-1840).
+void erasures8(unsigned K, unsigned R, unsigned m, const void* const* orig, const void* const* rec, uint32_t* erased) {
+    std::memset(erased, 0, 8 * sizeof(uint32_t));
+    auto set = [&](unsigned p) { erased[p >> 5] |= 1u << (p & 31); };
+    for (unsigned i = 0; i < R; ++i)
+        if (!rec[i]) set(i);
+    for (unsigned i = R; i < m; ++i) set(i);
+    for (unsigned i = 0; i < K; ++i)
+        if (!orig[i]) set(m + i);
+}
+
+// GF(2^8) decoder argument block of one object (columns [off, off + bytes));
+// returns true when the half-position decoder applies (no original survives
+// and n = 2m: every received piece is in the low half of the positions, every
+// output in the high half; k_ff8_dec_half, rs_ff8.hip).
+bool fill_dec8(Ff8DecArgs& a, const DeviceTables* t, unsigned K, unsigned R, const void* const* orig,
+               const void* const* rec, void** work, uint64_t off, uint64_t bytes) {
+    const unsigned m = next_pow2(R);
+    const unsigned Tn = log2u(next_pow2(m + K));
     std::memset(&a, 0, sizeof(a));
-    auto mark = [](uint32_t* pyr, unsigned p) {
-        for (unsigned L = 0; L <= 8; ++L) {
-            const unsigned j = p >> L;
-            pyr[pyr8_offset(L) + (j >> 5)] |= 1u << (j & 31);
-        }
-    };
-    auto set_ptrs = [&](uint64_t pos) {
-        auto addr = [&](const void* p) { return uint64_t(reinterpret_cast<uintptr_t>(p)) + off + pos; };
-        for (unsigned i = 0; i < R; ++i)
-            if (rec[i]) a.ptr[i] = addr(rec[i]);
-        for (unsigned i = 0; i < K; ++i)
-            a.ptr[m + i] = addr(orig[i] ? orig[i] : work[i]);  // lost: its slot carries the output
-    };
+    uint32_t erased[8];
+    erasures8(K, R, m, orig, rec, erased);
+    auto addr = [&](const void* p) { return uint64_t(reinterpret_cast<uintptr_t>(p)) + off; };
+    for (unsigned i = 0; i < R; ++i)
+        if (rec[i]) a.ptr[i] = addr(rec[i]);
+    for (unsigned i = 0; i < K; ++i) a.ptr[m + i] = addr(orig[i] ? orig[i] : work[i]);  // lost: its slot carries the output
     // The pyramids depend only on (K, R, erasure pattern); the last pattern is
     // cached per thread (repeated patterns are the common case).
     struct PyrCache {
@@ -493,7 +528,13 @@ LeopardResult decode_device8(Call& c, uint64_t bytes, uint64_t off, unsigned K, 
         uint32_t present[kPyr8Words], needed[kPyr8Words];
     };
     thread_local PyrCache pc;
-    if (pc.K != K || pc.R != R || std::memcmp(pc.erased, erased.data(), sizeof(pc.erased)) != 0) {
+    if (pc.K != K || pc.R != R || std::memcmp(pc.erased, erased, sizeof(pc.erased)) != 0) {
+        auto mark = [](uint32_t* pyr, unsigned p) {
+            for (unsigned L = 0; L <= 8; ++L) {
+                const unsigned j = p >> L;
+                pyr[pyr8_offset(L) + (j >> 5)] |= 1u << (j & 31);
+            }
+        };
         std::memset(pc.present, 0, sizeof(pc.present));
         std::memset(pc.needed, 0, sizeof(pc.needed));
         for (unsigned i = 0; i < R; ++i)
@@ -501,25 +542,30 @@ LeopardResult decode_device8(Call& c, uint64_t bytes, uint64_t off, unsigned K, 
         for (unsigned i = 0; i < K; ++i) mark(orig[i] ? pc.present : pc.needed, m + i);
         pc.K = K;
         pc.R = R;
-        std::memcpy(pc.erased, erased.data(), sizeof(pc.erased));
+        std::memcpy(pc.erased, erased, sizeof(pc.erased));
     }
     std::memcpy(a.present, pc.present, sizeof(a.present));
     std::memcpy(a.needed, pc.needed, sizeof(a.needed));
     error_locator8(erased, a.el);
-    a.sktab = c.t->sktab8;
-    a.tabs = c.t->tab8;
+    a.sktab = t->sktab8;
+    a.tabs = t->tab8;
     a.K = K;
     a.R = R;
     a.m = m;
-    // No original survives and n = 2m: every received piece is in the low half of
-    // the positions, every output in the high half (k_ff8_dec_half, rs_ff8.hip).
+    a.nunits = uint32_t(bytes / 4);
     bool any_orig = false;
     for (unsigned i = 0; i < K; ++i) any_orig |= orig[i] != nullptr;
     const bool half = !any_orig && Tn >= 2 && 2 * m == (1u << Tn) && ff8_half_decoder_enabled();
-    if (half) a.fused = c.t->fused8 + size_t(Tn - 2) * 256 * kTab8Dwords;  // T = Tn - 1, chunk 0
+    if (half) a.fused = t->fused8 + size_t(Tn - 2) * 256 * kTab8Dwords;  // T = Tn - 1, chunk 0
+    return half;
+}
+
+LeopardResult decode_device8(Call& c, uint64_t bytes, uint64_t off, unsigned K, unsigned R, const void* const* orig,
+                             const void* const* rec, void** work) {
+    const unsigned Tn = log2u(next_pow2(next_pow2(R) + K));
+    Ff8DecArgs a;
     for (uint64_t pos = 0; pos < bytes; pos += kFf8MaxLaunchBytes) {  // see encode_device
-        set_ptrs(pos);
-        a.nunits = uint32_t(std::min(kFf8MaxLaunchBytes, bytes - pos) / 4);
+        const bool half = fill_dec8(a, c.t, K, R, orig, rec, work, off + pos, std::min(kFf8MaxLaunchBytes, bytes - pos));
         HIP_OK(half ? launch_ff8_decode_half(Tn - 1, a, c.s) : launch_ff8_decode(Tn, a, c.s), "decode kernel");
     }
     return Leopard_Success;
@@ -531,6 +577,7 @@ LeopardResult decode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
     const unsigned n = next_pow2(m + K);
     const bool ff16 = n > 256;
     const unsigned Tn = log2u(n);
+    if (!ff16) return decode_device8(c, bytes, off, K, R, orig, rec, work);
 
     // error_locations[] = 1 at lost recoveries, [R, m), lost originals (LeopardFF8.cpp:1825-1840)
     std::vector<uint32_t> erased((std::max(n, 256u) + 31) / 32, 0);
@@ -541,7 +588,7 @@ LeopardResult decode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
     for (unsigned i = 0; i < K; ++i)
         if (!orig[i]) set(m + i);
 
-    if (!ff16) return decode_device8(c, bytes, off, K, R, m, Tn, orig, rec, work, erased);
+
 
     DecArgs a;
     std::memset(&a, 0, sizeof(a));
@@ -584,17 +631,11 @@ LeopardResult decode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
     const size_t off_slab = table_bytes;
     LeopardResult r = ws.reserve_device(off_slab + slab_pieces * slice);
     if (r != Leopard_Success) return r;
-    // one staging image: piece tables (if any) then, on a new pattern, bitmap + pyramids
-    const size_t stage_bytes = table_bytes + (rebuild ? off_tmp : 0);
-    if (stage_bytes) {
-        r = ws.reserve_stage(stage_bytes);
-        if (r != Leopard_Success) return r;
-        if (!mb.staged.empty()) {
-            std::memcpy(ws.hstage, mb.staged.data(), mb.bytes());
-            HIP_OK(hipMemcpyAsync(ws.dbuf, ws.hstage, mb.bytes(), hipMemcpyHostToDevice, c.s), "upload piece tables");
-        }
-        if (rebuild) {
-            uint8_t* h = ws.hstage + table_bytes;
+    // piece tables (if any), and on a new pattern the bitmap + pyramids
+    r = mb.flush(ws, reinterpret_cast<uint64_t*>(ws.dbuf), c.s);
+    if (r != Leopard_Success) return r;
+    if (rebuild) {
+        r = ws.upload(ws.dec16, off_tmp, c.s, [&](uint8_t* h) {
             std::memset(h, 0, off_tmp);
             std::memcpy(h, erased.data(), erased.size() * 4);
             uint32_t* pp = reinterpret_cast<uint32_t*>(h + off_pyr);
@@ -608,12 +649,9 @@ LeopardResult decode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
             for (unsigned i = 0; i < R; ++i)
                 if (rec[i]) mark(pp, i);
             for (unsigned i = 0; i < K; ++i) mark(orig[i] ? pp : pn, m + i);
-            HIP_OK(hipMemcpyAsync(ws.dec16, h, off_tmp, hipMemcpyHostToDevice, c.s), "upload decode state");
-        }
-        HIP_OK(hipEventRecord(ws.stage_done, c.s), "record staging");
-        ws.stage_pending = true;
+        });
+        if (r != Leopard_Success) return r;
     }
-    for (auto& p : mb.pending) p.map->table = reinterpret_cast<uint64_t*>(ws.dbuf) + p.index;
 
     uint32_t* d_bitmap = reinterpret_cast<uint32_t*>(ws.dec16);
     uint32_t* d_tmp = reinterpret_cast<uint32_t*>(ws.dec16 + off_tmp);
@@ -1026,6 +1064,124 @@ LeopardResult decode_checked(uint64_t bytes, uint64_t off, unsigned K, unsigned 
     return decode_any(bytes, off, K, R, orig, rec, work);
 }
 
+// ------------------------------------------------------------- batches ----
+
+// leo_amd_encode_batch / leo_amd_decode_batch: `count` independent objects of
+// one shape, each with exactly the semantics of one leo_encode / leo_decode.
+// Device-resident GF(2^8) objects on one device run as ONE launch over every
+// object's column strips (argument blocks uploaded through the staging ring),
+// so a batch of small objects fills the GPU where a single 64 KiB-piece call
+// gives each CU one workgroup; anything else runs object by object.
+bool batch_on_device(unsigned count, const void* const* firsts, int* dev) {
+    MemKind kind;
+    *dev = pick_device(firsts[0], &kind);
+    if (kind != MemKind::Device) return false;
+    for (unsigned o = 1; o < count; ++o) {
+        int d = -1;
+        if (classify(firsts[o], &d) != MemKind::Device || d != *dev) return false;
+    }
+    return true;
+}
+
+template <class Args, class Fill, class Launch>
+LeopardResult run_batch8(int dev, unsigned count, Fill fill, Launch launch) {
+    DeviceGuard guard(dev);
+    Call c;
+    LeopardResult r = begin_call(dev, c);
+    if (r != Leopard_Success) return r;
+    const size_t bytes = size_t(count) * sizeof(Args);
+    r = c.ws->reserve_device(bytes);
+    if (r != Leopard_Success) return r;
+    Args* dargs = reinterpret_cast<Args*>(c.ws->dbuf);
+    bool all_flag = true;
+    r = c.ws->upload(dargs, bytes, c.s, [&](uint8_t* h) {
+        Args* ha = reinterpret_cast<Args*>(h);
+        for (unsigned o = 0; o < count; ++o) all_flag &= fill(ha[o], c.t, o);
+    });
+    if (r != Leopard_Success) return r;
+    HIP_OK(launch(dargs, all_flag, c.s), "batch kernel");
+    return finish(c, false);
+}
+
+LeopardResult encode_batch(unsigned count, uint64_t bytes, unsigned K, unsigned R, unsigned work_count,
+                           const void* const* const* orig, void** const* work) {
+    if (!orig || !work) return Leopard_InvalidInput;
+    for (unsigned o = 0; o < count; ++o) {
+        const LeopardResult r = check_encode(bytes, K, R, work_count, orig[o], work[o]);
+        if (r != Leopard_Success) return r;
+    }
+    if (count == 0) return Leopard_Success;
+    const unsigned m = next_pow2(R), n = next_pow2(m + K);
+    std::vector<const void*> firsts(count);
+    for (unsigned o = 0; o < count; ++o) firsts[o] = orig[o][0];
+    int dev = -1;
+    if (K > 1 && R > 1 && n <= 256 && bytes <= kFf8MaxLaunchBytes && batch_on_device(count, firsts.data(), &dev)) {
+        const unsigned Tm = log2u(m);
+        return run_batch8<Ff8EncArgs>(
+            dev, count,
+            [&](Ff8EncArgs& a, const DeviceTables* t, unsigned o) {
+                fill_enc8(a, t, K, R, orig[o], work[o], 0, bytes);
+                return true;
+            },
+            [&](const Ff8EncArgs* d, bool, hipStream_t s) {
+                return launch_ff8_encode_batch(Tm, d, count, uint32_t(bytes / 4), (K + m - 1) / m > 1, s);
+            });
+    }
+    for (unsigned o = 0; o < count; ++o) {
+        const LeopardResult r = encode_any(bytes, 0, K, R, orig[o], work[o]);
+        if (r != Leopard_Success) return r;
+    }
+    return Leopard_Success;
+}
+
+LeopardResult decode_batch(unsigned count, uint64_t bytes, unsigned K, unsigned R, unsigned work_count,
+                           const void* const* const* orig, const void* const* const* rec, void** const* work) {
+    if (!orig || !rec || !work) return Leopard_InvalidInput;
+    bool general = true;  // every object takes the general decoder (no edge path)
+    for (unsigned o = 0; o < count; ++o) {
+        LeopardResult r = check_decode(bytes, K, R, work_count, orig[o], rec[o], work[o]);
+        if (r != Leopard_Success) return r;
+        unsigned lost = 0, got = 0;
+        for (unsigned i = 0; i < K; ++i) lost += orig[o][i] == nullptr;
+        for (unsigned i = 0; i < R; ++i) got += rec[o][i] != nullptr;
+        if (got < lost) return Leopard_NeedMoreData;
+        if (K == 1 || lost == 0 || R == 1) {
+            general = false;
+        } else {
+            const unsigned n = next_pow2(next_pow2(R) + K);
+            if (work_count != n) return Leopard_InvalidCounts;
+            if (n > 65536) return Leopard_TooMuchData;
+        }
+    }
+    if (count == 0) return Leopard_Success;
+    const unsigned m = next_pow2(R), n = next_pow2(m + K);
+    int dev = -1;
+    if (general && n <= 256 && bytes <= kFf8MaxLaunchBytes) {
+        std::vector<const void*> firsts(count);
+        for (unsigned o = 0; o < count; ++o) {
+            const void* f = nullptr;
+            for (unsigned i = 0; i < R && !f; ++i) f = rec[o][i];
+            firsts[o] = f;
+        }
+        if (batch_on_device(count, firsts.data(), &dev)) {
+            const unsigned Tn = log2u(n);
+            return run_batch8<Ff8DecArgs>(
+                dev, count,
+                [&](Ff8DecArgs& a, const DeviceTables* t, unsigned o) {
+                    return fill_dec8(a, t, K, R, orig[o], rec[o], work[o], 0, bytes);
+                },
+                [&](const Ff8DecArgs* d, bool half, hipStream_t s) {
+                    return launch_ff8_decode_batch(half ? Tn - 1 : Tn, d, count, uint32_t(bytes / 4), half, s);
+                });
+        }
+    }
+    for (unsigned o = 0; o < count; ++o) {
+        const LeopardResult r = decode_any(bytes, 0, K, R, orig[o], rec[o], work[o]);
+        if (r != Leopard_Success) return r;
+    }
+    return Leopard_Success;
+}
+
 }  // namespace
 }  // namespace lamd
 
@@ -1131,6 +1287,21 @@ LEO_EXPORT LeopardResult leo_amd_decode_slice(uint64_t buffer_bytes, uint64_t by
     if (r != Leopard_Success) return r;
     return decode_checked(slice_bytes, byte_offset, original_count, recovery_count, work_count, original_data,
                           recovery_data, work_data);
+}
+
+LEO_EXPORT LeopardResult leo_amd_encode_batch(unsigned object_count, uint64_t buffer_bytes, unsigned original_count,
+                                              unsigned recovery_count, unsigned work_count,
+                                              const void* const* const* original_data, void** const* work_data) {
+    return encode_batch(object_count, buffer_bytes, original_count, recovery_count, work_count, original_data,
+                        work_data);
+}
+
+LEO_EXPORT LeopardResult leo_amd_decode_batch(unsigned object_count, uint64_t buffer_bytes, unsigned original_count,
+                                              unsigned recovery_count, unsigned work_count,
+                                              const void* const* const* original_data,
+                                              const void* const* const* recovery_data, void** const* work_data) {
+    return decode_batch(object_count, buffer_bytes, original_count, recovery_count, work_count, original_data,
+                        recovery_data, work_data);
 }
 
 LEO_EXPORT void leo_amd_set_stream(void* hip_stream) { tls.stream = static_cast<hipStream_t>(hip_stream); }

@@ -94,6 +94,14 @@ hipError_t launch_error_locator16(const uint32_t* erased, const uint32_t* walsh,
 hipError_t launch_xor_reduce(const XorArgs& a, hipStream_t s);
 hipError_t launch_ff8_encode(unsigned T, const Ff8EncArgs& a, hipStream_t s);
 hipError_t launch_ff8_decode(unsigned T, const Ff8DecArgs& a, hipStream_t s);
+// Batched GF(2^8) launches: `count` argument blocks in device memory (same T,
+// column count and chunk structure), one grid (strips x objects).  For the
+// decoder, half = every object qualifies for k_ff8_dec_half (T is then the
+// half tile's bits, as for launch_ff8_decode_half).
+hipError_t launch_ff8_encode_batch(unsigned T, const Ff8EncArgs* objs, unsigned count, uint32_t nunits, bool multi,
+                                   hipStream_t s);
+hipError_t launch_ff8_decode_batch(unsigned T, const Ff8DecArgs* objs, unsigned count, uint32_t nunits, bool half,
+                                   hipStream_t s);
 
 // Units per lane chosen for each kernel family (the host sizes grids with it).
 constexpr int kUnitsPerLane = 1;

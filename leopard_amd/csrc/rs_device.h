@@ -37,6 +37,9 @@
 #ifndef LAMD_FF16_PREFETCH
 #define LAMD_FF16_PREFETCH 0
 #endif
+#ifndef LAMD_FF16_INFLIGHT  // GF(2^16) butterflies a wave keeps in flight (scheduling window)
+#define LAMD_FF16_INFLIGHT 2
+#endif
 
 namespace lamd {
 
@@ -145,11 +148,19 @@ struct FF16 {
         ph = xor3(perm(t[3], t[2], a0), perm(t[7], t[6], a1), perm(t[11], t[10], b0));
         ph = xor3(ph, perm(t[15], t[14], b1), perm(t[17], t[17], a2)) ^ perm(t[19], t[19], b2);
     }
-    LDEV static void muladd(uint32_t* x, const uint32_t* y, const Tab& t) {
-        uint32_t pl, ph;
-        prod(y[0], y[1], t, pl, ph);
-        x[0] ^= pl;
-        x[1] ^= ph;
+    // x ^= y * c: the six products of each output byte and x folded by three
+    // 3-input XORs (v_bitop3) per output dword.  (v_perm_b32 issues at half the
+    // rate of a VOP2 op on gfx950, tools/ubench_isa2.hip: the 12 perms are half
+    // of a butterfly's issue time, the selectors and XORs the other half.)
+    LDEV static void muladd(uint32_t* x, const uint32_t* y, const Tab& T) {
+        const uint32_t lo = y[0], hi = y[1];
+        const uint32_t a0 = lo & 0x07070707u, a1 = (lo >> 3) & 0x07070707u, a2 = (lo >> 6) & 0x03030303u;
+        const uint32_t b0 = hi & 0x07070707u, b1 = (hi >> 3) & 0x07070707u, b2 = (hi >> 6) & 0x03030303u;
+        const uint32_t* t = T.t;
+        x[0] = xor3(x[0], xor3(perm(t[1], t[0], a0), perm(t[5], t[4], a1), perm(t[9], t[8], b0)),
+                    xor3(perm(t[13], t[12], b1), perm(t[16], t[16], a2), perm(t[18], t[18], b2)));
+        x[1] = xor3(x[1], xor3(perm(t[3], t[2], a0), perm(t[7], t[6], a1), perm(t[11], t[10], b0)),
+                    xor3(perm(t[15], t[14], b1), perm(t[17], t[17], a2), perm(t[19], t[19], b2)));
     }
     LDEV static void mul(uint32_t* x, const uint32_t* y, const Tab& t) { prod(y[0], y[1], t, x[0], x[1]); }
 };
@@ -588,7 +599,7 @@ struct Tile {
                         // ~10 temporaries next to a 64-VGPR tile and its table)
 #pragma unroll
                         for (int k = 0; k < F::kDw; ++k) asm volatile("" : "+v"(a[k]), "+v"(b[k]));
-                        if ((j * C + u) & 1) __builtin_amdgcn_sched_barrier(0);
+                        if ((j * C + u) % LAMD_FF16_INFLIGHT == LAMD_FF16_INFLIGHT - 1) __builtin_amdgcn_sched_barrier(0);
                     }
                 }
             }
@@ -613,14 +624,22 @@ struct Tile {
             });
         } else {
 #if LAMD_FF16_PREFETCH
-            // FF16 (20-dword tables in SGPRs): software pipeline, two tables live.
+            // FF16: software pipeline, the next group's table read is issued
+            // ahead of this group's butterflies (two tables live).
             typename F::Tab next = table(0);
             static_for<0, NG>([&](auto GI) {
                 constexpr int g = decltype(GI)::value * 2 * half;
                 const typename F::Tab t = next;
+                asm volatile("" ::: "memory");
                 if constexpr (g + 2 * half < NR) next = table(g + 2 * half);
                 __builtin_amdgcn_sched_barrier(0);
-                if (live(g)) group(g, t);
+                if (live(g)) {
+                    group(g, t);
+#pragma unroll
+                    for (int j = 0; j < 2 * half; ++j)
+#pragma unroll
+                        for (int k = 0; k < U; ++k) asm volatile("" : "+v"(x[g + j][k]));
+                }
                 __builtin_amdgcn_sched_barrier(0);
             });
 #else

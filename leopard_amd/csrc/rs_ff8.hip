@@ -150,7 +150,7 @@ LDEV auto lane_pred(const P& p) {
 }
 
 template <int T, int RB, bool kMulti, int NA, int G>
-__global__ void __launch_bounds__(threads_for(T, RB) >> G, 4) k_ff8_enc(Ff8EncArgs a) {
+LDEV void ff8_enc(const Ff8EncArgs& a) {
     if constexpr ((LAMD_ABLATE & 16) != 0) return;
     // G lane-group bits: the wave's 64 lanes hold 2^G column strips of LW lanes
     // for different pieces (virtual wave w = lane group above the real wave), so
@@ -255,6 +255,18 @@ __global__ void __launch_bounds__(threads_for(T, RB) >> G, 4) k_ff8_enc(Ff8EncAr
     STAMP(5);
 }
 
+template <int T, int RB, bool kMulti, int NA, int G>
+__global__ void __launch_bounds__(threads_for(T, RB) >> G, 4) k_ff8_enc(Ff8EncArgs a) {
+    ff8_enc<T, RB, kMulti, NA, G>(a);
+}
+// Batched launch (leo_amd_encode_batch): object blockIdx.y of an array of
+// argument blocks in device memory (read through the scalar cache like the
+// kernel arguments of k_ff8_enc); one grid over every object's column strips.
+template <int T, int RB, bool kMulti>
+__global__ void __launch_bounds__(threads_for(T, RB), 4) k_ff8_enc_batch(const Ff8EncArgs* __restrict__ objs) {
+    ff8_enc<T, RB, kMulti, 1, 0>(objs[blockIdx.y]);
+}
+
 // --------------------------------------------------------------- decode -----
 
 LDEV unsigned el_at(const Ff8DecArgs& a, unsigned p) { return (a.el[p >> 2] >> ((p & 3) * 8)) & 0xFFu; }
@@ -277,7 +289,7 @@ LDEV void scale_batched(typename TL::Reg& v, const LdsTab8<256>& ltab, LogFn log
 }
 
 template <int T, int RB, int NA>
-__global__ void __launch_bounds__(threads_for(T, RB), 4) k_ff8_dec(Ff8DecArgs a) {
+LDEV void ff8_dec(const Ff8DecArgs& a) {
     if constexpr ((LAMD_ABLATE & 16) != 0) return;
     using F = FF8;
     using TL = Tile<F, T, RB, 1>;
@@ -339,6 +351,14 @@ __global__ void __launch_bounds__(threads_for(T, RB), 4) k_ff8_dec(Ff8DecArgs a)
         if (is_needed(r)) gstore(pp[r], cl, v[r][0]);
     STAMP(6);
 }
+template <int T, int RB, int NA>
+__global__ void __launch_bounds__(threads_for(T, RB), 4) k_ff8_dec(Ff8DecArgs a) {
+    ff8_dec<T, RB, NA>(a);
+}
+template <int T, int RB>
+__global__ void __launch_bounds__(threads_for(T, RB), 4) k_ff8_dec_batch(const Ff8DecArgs* __restrict__ objs) {
+    ff8_dec<T, RB, 1>(objs[blockIdx.y]);
+}
 
 // Decode when every received piece sits in the low half of the positions (no
 // original survives; n = 2m, so recovery [0, R) is the low half and the lost
@@ -352,7 +372,7 @@ __global__ void __launch_bounds__(threads_for(T, RB), 4) k_ff8_dec(Ff8DecArgs a)
 // the top layers fuse as in the encoder), no derivative, every wave busy (in k_ff8_dec the waves of the
 // empty high half idle through the scale and the low IFFT layers).
 template <int T, int RB>
-__global__ void __launch_bounds__(threads_for(T, RB), 4) k_ff8_dec_half(Ff8DecArgs a) {
+LDEV void ff8_dec_half(const Ff8DecArgs& a) {
     if constexpr ((LAMD_ABLATE & 16) != 0) return;
     using F = FF8;
     using TL = Tile<F, T, RB, 1>;
@@ -397,6 +417,14 @@ __global__ void __launch_bounds__(threads_for(T, RB), 4) k_ff8_dec_half(Ff8DecAr
     for (int r = 0; r < TL::NR; ++r)
         if (is_needed(r)) gstore(pp[r], cl, v[r][0]);
 }
+template <int T, int RB>
+__global__ void __launch_bounds__(threads_for(T, RB), 4) k_ff8_dec_half(Ff8DecArgs a) {
+    ff8_dec_half<T, RB>(a);
+}
+template <int T, int RB>
+__global__ void __launch_bounds__(threads_for(T, RB), 4) k_ff8_dec_half_batch(const Ff8DecArgs* __restrict__ objs) {
+    ff8_dec_half<T, RB>(objs[blockIdx.y]);
+}
 
 // Opting a kernel into > 64 KiB of LDS is a per-function attribute, set once
 // per kernel (Once is a distinct type per kernel instantiation).
@@ -420,6 +448,26 @@ hipError_t launch8(KernelFn* fn, unsigned threads, const Args& a, size_t lds_dwo
     const dim3 grid((a.nunits + lw - 1) / lw);
     return hipLaunchKernel(reinterpret_cast<const void*>(fn), grid, dim3(threads), params, lds, s);
 }
+// Batched form: argument blocks in device memory, grid (strips, objects).
+template <class Tag, class KernelFn, class Args>
+hipError_t launch8_batch(KernelFn* fn, unsigned threads, const Args* objs, unsigned count, uint32_t nunits,
+                         size_t lds_dwords, hipStream_t s) {
+    const size_t lds = lds_dwords * 4;
+    if (lds > 65536) {
+        const hipError_t e = Once<Tag>::set_lds(reinterpret_cast<const void*>(fn), lds);
+        if (e != hipSuccess) return e;
+    }
+    const Args* arg = objs;
+    void* params[] = {&arg};
+    return hipLaunchKernel(reinterpret_cast<const void*>(fn), dim3((nunits + 63) / 64, count), dim3(threads), params,
+                           lds, s);
+}
+template <int T, bool M>
+struct EncBatchTag {};
+template <int T>
+struct DecBatchTag {};
+template <int T>
+struct DecHalfBatchTag {};
 
 template <int T, int RB, bool M, int NA, int G>
 struct EncTag {};
@@ -517,6 +565,46 @@ hipError_t launch_ff8_decode_half(unsigned Tm, const Ff8DecArgs& a, hipStream_t 
     hipError_t e = hipErrorInvalidValue;
     static_for<1, 8>([&](auto I) {
         if (Tm == unsigned(decltype(I)::value)) e = dec_half_T<decltype(I)::value>(a, s);
+    });
+    return e;
+}
+
+hipError_t launch_ff8_encode_batch(unsigned T, const Ff8EncArgs* objs, unsigned count, uint32_t nunits, bool multi,
+                                   hipStream_t s) {
+    hipError_t e = hipErrorInvalidValue;
+    static_for<1, 8>([&](auto I) {
+        constexpr int TT = decltype(I)::value, RB = reg_bits8(TT);
+        constexpr size_t lds = tile_dwords_for(TT, RB) + LdsTab8<256>::kDwords;
+        if (T != unsigned(TT)) return;
+        if (multi)
+            e = launch8_batch<EncBatchTag<TT, true>>(&k_ff8_enc_batch<TT, RB, true>, threads_for(TT, RB), objs, count,
+                                                     nunits, lds, s);
+        else
+            e = launch8_batch<EncBatchTag<TT, false>>(&k_ff8_enc_batch<TT, RB, false>, threads_for(TT, RB), objs,
+                                                      count, nunits, lds, s);
+    });
+    return e;
+}
+
+hipError_t launch_ff8_decode_batch(unsigned T, const Ff8DecArgs* objs, unsigned count, uint32_t nunits, bool half,
+                                   hipStream_t s) {
+    hipError_t e = hipErrorInvalidValue;
+    if (half) {
+        static_for<1, 8>([&](auto I) {
+            constexpr int TT = decltype(I)::value, RB = reg_bits8(TT);
+            constexpr size_t lds = tile_dwords_for(TT, RB) + 2 * LdsTab8<256>::kDwords;
+            if (T == unsigned(TT))
+                e = launch8_batch<DecHalfBatchTag<TT>>(&k_ff8_dec_half_batch<TT, RB>, threads_for(TT, RB), objs, count,
+                                                       nunits, lds, s);
+        });
+        return e;
+    }
+    static_for<1, 9>([&](auto I) {
+        constexpr int TT = decltype(I)::value, RB = reg_bits8(TT);
+        constexpr size_t lds = tile_dwords_for(TT, RB) + 2 * LdsTab8<256>::kDwords;
+        if (T == unsigned(TT))
+            e = launch8_batch<DecBatchTag<TT>>(&k_ff8_dec_batch<TT, RB>, threads_for(TT, RB), objs, count, nunits, lds,
+                                               s);
     });
     return e;
 }

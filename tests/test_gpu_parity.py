@@ -473,3 +473,80 @@ def test_async_calls_on_two_streams_do_not_share_scratch(leo):
         dw = job["dwork"].cpu().numpy()
         for i in job["lo"]:
             assert np.array_equal(dw[i], job["data"][i]), (job["k"], r, i)
+
+
+# ------------------------------------------------------------- batches --
+
+def _batch_objects(k, r, b, count, seed):
+    rng = np.random.default_rng(seed)
+    return [rng.integers(0, 256, (k, b), dtype=np.uint8) for _ in range(count)]
+
+
+@pytest.mark.parametrize("k,r,b", [(128, 128, 4096), (100, 20, 64 * 37), (200, 55, 1024), (1000, 200, 256)])
+def test_batch_encode_decode_match_oracle(leo, k, r, b):
+    """leo_amd_encode_batch / decode_batch (one launch over every object for
+    GF(2^8); object by object otherwise) == independent calls == the oracle.
+    The decode batch mixes erasure patterns: full loss (half-position
+    decoder), partial losses, and objects with lost recovery pieces."""
+    count = 5
+    objs = _batch_objects(k, r, b, count, k + r)
+    dev = [dev_tensor(d) for d in objs]
+    wc, dwc = leo.leo_encode_work_count(k, r), leo.leo_decode_work_count(k, r)
+    works = [torch.zeros((wc, b), dtype=torch.uint8, device="cuda") for _ in range(count)]
+    res = leo.leo_amd_encode_batch(b, k, r, wc, [[t[i].data_ptr() for i in range(k)] for t in dev],
+                                   [[w[i].data_ptr() for i in range(wc)] for w in works])
+    assert res == leo.LeopardResult.Success, leo.last_error()
+    torch.cuda.synchronize()
+    recs = [w[:r].cpu().numpy() for w in works]
+    for d, rec in zip(objs, recs):
+        assert np.array_equal(rec, ol.oracle().encode(d, r))
+    rng = np.random.default_rng(7)
+    pats = []
+    for o in range(count):
+        loss = min(k, r) if o % 2 == 0 else int(rng.integers(1, min(k, r) + 1))
+        lo = sorted(rng.choice(k, loss, replace=False).tolist())
+        lr = sorted(rng.choice(r, r - loss, replace=False).tolist())
+        pats.append((set(lo), set(lr)))
+    dworks = [torch.zeros((dwc, b), dtype=torch.uint8, device="cuda") for _ in range(count)]
+    recd = [dev_tensor(x) for x in recs]
+    res = leo.leo_amd_decode_batch(
+        b, k, r, dwc, [[None if i in lo else dev[o][i].data_ptr() for i in range(k)] for o, (lo, _) in enumerate(pats)],
+        [[None if i in lr else recd[o][i].data_ptr() for i in range(r)] for o, (_, lr) in enumerate(pats)],
+        [[w[i].data_ptr() for i in range(dwc)] for w in dworks])
+    assert res == leo.LeopardResult.Success, leo.last_error()
+    torch.cuda.synchronize()
+    for o, (lo, _) in enumerate(pats):
+        got = dworks[o].cpu().numpy()
+        for i in lo:
+            assert np.array_equal(got[i], objs[o][i]), (o, i)
+
+
+def test_batch_full_loss_and_validation(leo):
+    """The benchmark's batch (every original lost, the half-position decoder in
+    one launch) and the batch validation rules."""
+    k = r = 128
+    b = 2048
+    count = 4
+    objs = _batch_objects(k, r, b, count, 3)
+    dev = [dev_tensor(d) for d in objs]
+    wc, dwc = leo.leo_encode_work_count(k, r), leo.leo_decode_work_count(k, r)
+    works = [torch.zeros((wc, b), dtype=torch.uint8, device="cuda") for _ in range(count)]
+    po = [[t[i].data_ptr() for i in range(k)] for t in dev]
+    pw = [[w[i].data_ptr() for i in range(wc)] for w in works]
+    assert leo.leo_amd_encode_batch(b, k, r, wc, po, pw) == leo.LeopardResult.Success
+    dworks = [torch.zeros((dwc, b), dtype=torch.uint8, device="cuda") for _ in range(count)]
+    pr = [[w[i].data_ptr() for i in range(r)] for w in works]
+    pd = [[w[i].data_ptr() for i in range(dwc)] for w in dworks]
+    assert leo.leo_amd_decode_batch(b, k, r, dwc, [[None] * k] * count, pr, pd) == leo.LeopardResult.Success
+    torch.cuda.synchronize()
+    for o in range(count):
+        assert torch.equal(dworks[o][:k], dev[o])
+    R = leo.LeopardResult
+    # every object is validated before anything runs
+    assert leo.leo_amd_encode_batch(b, k, r, wc - 1, po, pw) == R.InvalidCounts
+    assert leo.leo_amd_encode_batch(b + 1, k, r, wc, po, pw) == R.InvalidSize
+    short = [[None] * k] * count
+    pr_bad = [list(x) for x in pr]
+    pr_bad[2] = [None] * r  # object 2 received nothing
+    assert leo.leo_amd_decode_batch(b, k, r, dwc, short, pr_bad, pd) == R.NeedMoreData
+    assert leo.leo_amd_encode_batch(b, k, r, wc, [], []) == R.Success

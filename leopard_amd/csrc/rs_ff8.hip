@@ -57,6 +57,15 @@ constexpr int wide_bits8(int T) { return T == 7 ? 4 : reg_bits8(T); }
 constexpr unsigned threads_for(int T, int RB) { return 64u << (T - RB); }
 constexpr size_t tile_dwords_for(int T, int RB) { return T > RB ? (size_t(1) << T) * 64 : 0; }
 constexpr int wide_dec_bits8(int T) { return T == 8 ? 5 : reg_bits8(T); }
+// Batched launches hold many workgroups per CU: their 7- and 8-bit tiles use
+// 16 / 32 pieces per lane (8-wave workgroups, one transpose per transform,
+// four workgroups per CU).  Measured, 16 objects of 128+128 x 64 KiB per
+// batch: 632 GB/s vs 557 with the 16-wave tiles of the single calls and 532
+// with 32 pieces per lane (LAMD_BATCH_BITS8 = 3 / 5; 0 = the single-call tiles).
+#ifndef LAMD_BATCH_BITS8
+#define LAMD_BATCH_BITS8 4
+#endif
+constexpr int batch_bits8(int T) { return LAMD_BATCH_BITS8 && T >= 7 ? LAMD_BATCH_BITS8 : reg_bits8(T); }
 
 // Transforms: the plain ones (Tile::ifft / fft: one LDS area, two barriers
 // per exchange) by default; LAMD_FF8_PIPE=1 builds the pipelined ones
@@ -573,7 +582,7 @@ hipError_t launch_ff8_encode_batch(unsigned T, const Ff8EncArgs* objs, unsigned 
                                    hipStream_t s) {
     hipError_t e = hipErrorInvalidValue;
     static_for<1, 8>([&](auto I) {
-        constexpr int TT = decltype(I)::value, RB = reg_bits8(TT);
+        constexpr int TT = decltype(I)::value, RB = batch_bits8(TT);
         constexpr size_t lds = tile_dwords_for(TT, RB) + LdsTab8<256>::kDwords;
         if (T != unsigned(TT)) return;
         if (multi)
@@ -591,7 +600,7 @@ hipError_t launch_ff8_decode_batch(unsigned T, const Ff8DecArgs* objs, unsigned 
     hipError_t e = hipErrorInvalidValue;
     if (half) {
         static_for<1, 8>([&](auto I) {
-            constexpr int TT = decltype(I)::value, RB = reg_bits8(TT);
+            constexpr int TT = decltype(I)::value, RB = batch_bits8(TT);
             constexpr size_t lds = tile_dwords_for(TT, RB) + 2 * LdsTab8<256>::kDwords;
             if (T == unsigned(TT))
                 e = launch8_batch<DecHalfBatchTag<TT>>(&k_ff8_dec_half_batch<TT, RB>, threads_for(TT, RB), objs, count,
@@ -600,7 +609,7 @@ hipError_t launch_ff8_decode_batch(unsigned T, const Ff8DecArgs* objs, unsigned 
         return e;
     }
     static_for<1, 9>([&](auto I) {
-        constexpr int TT = decltype(I)::value, RB = reg_bits8(TT);
+        constexpr int TT = decltype(I)::value, RB = batch_bits8(TT);
         constexpr size_t lds = tile_dwords_for(TT, RB) + 2 * LdsTab8<256>::kDwords;
         if (T == unsigned(TT))
             e = launch8_batch<DecBatchTag<TT>>(&k_ff8_dec_batch<TT, RB>, threads_for(TT, RB), objs, count, nunits, lds,

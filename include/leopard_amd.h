@@ -29,6 +29,14 @@ LEO_EXPORT void leo_amd_set_async(int async_enable);
  * device at call time).  -1 restores the default.  Per thread. */
 LEO_EXPORT void leo_amd_set_device(int device);
 
+/* Host-memory calls of the calling thread split their columns into `ranges`
+ * 64-byte-aligned ranges, range i coded on device i % device_count by its own
+ * worker thread over that device's PCIe link; the call returns when all are
+ * done.  -1 = one range per device; 0 = the LEO_AMD_FANOUT environment value
+ * (default 1, no split).  At most one range per 4 KiB of columns.  Device
+ * pointers are not affected.  Per thread. */
+LEO_EXPORT void leo_amd_set_fanout(int ranges);
+
 /* Encode/decode a column range of every piece: identical to leo_encode /
  * leo_decode over bytes [byte_offset, byte_offset + slice_bytes) of each
  * piece (both multiples of 64).  This is how independent GPUs shard one object
@@ -61,6 +69,16 @@ LEO_EXPORT LeopardResult leo_amd_decode_batch(
     unsigned object_count, uint64_t buffer_bytes, unsigned original_count, unsigned recovery_count,
     unsigned work_count, const void* const* const* original_data, const void* const* const* recovery_data,
     void** const* work_data);
+
+/* Caller-registered host memory: pins [ptr, ptr + bytes) and maps it for
+ * every device.  leo_encode / leo_decode calls whose host pieces all lie in
+ * registered ranges run the kernels on them in place (reads and writes over
+ * PCIe, no staging copies); other host pieces go through the pinned staging
+ * pipeline.  The range must stay allocated until leo_amd_unregister_host(ptr)
+ * (the contract of hipHostRegister and RDMA memory registration).
+ * Returns Leopard_Platform when the runtime refuses the registration. */
+LEO_EXPORT LeopardResult leo_amd_register_host(void* ptr, uint64_t bytes);
+LEO_EXPORT LeopardResult leo_amd_unregister_host(void* ptr);
 
 /* Number of HIP devices usable by the library (0 when none / not gfx950). */
 LEO_EXPORT int leo_amd_device_count(void);

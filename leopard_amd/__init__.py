@@ -34,7 +34,7 @@ LEO_VERSION = 2
 __all__ = [
     "LEO_VERSION", "LeopardResult", "leo_init", "leo_result_string", "leo_encode_work_count", "leo_encode",
     "leo_decode_work_count", "leo_decode", "leo_amd_encode_slice", "leo_amd_decode_slice", "leo_amd_encode_batch",
-    "leo_amd_decode_batch", "set_stream",
+    "leo_amd_decode_batch", "register_host", "unregister_host", "set_fanout", "set_stream",
     "set_async", "set_device", "device_count", "table", "last_error", "encode", "decode", "LIB_PATH", "lib",
 ]
 
@@ -72,9 +72,12 @@ def _load():
         "leo_amd_decode_slice": (i, [u64, u64, u64, u, u, u, pp, pp, pp]),
         "leo_amd_encode_batch": (i, [u, u64, u, u, u, ctypes.POINTER(pp), ctypes.POINTER(pp)]),
         "leo_amd_decode_batch": (i, [u, u64, u, u, u, ctypes.POINTER(pp), ctypes.POINTER(pp), ctypes.POINTER(pp)]),
+        "leo_amd_register_host": (i, [vp, u64]),
+        "leo_amd_unregister_host": (i, [vp]),
         "leo_amd_set_stream": (None, [vp]),
         "leo_amd_set_async": (None, [i]),
         "leo_amd_set_device": (None, [i]),
+        "leo_amd_set_fanout": (None, [i]),
         "leo_amd_device_count": (i, []),
         "leo_amd_table": (i, [i, i, vp, u]),
         "leo_amd_last_error": (ctypes.c_char_p, []),
@@ -163,6 +166,15 @@ def leo_amd_decode_batch(buffer_bytes, original_count, recovery_count, work_coun
                                                   _ptr_arrays(work_data)))
 
 
+def register_host(ptr: int, nbytes: int) -> LeopardResult:
+    """Pin + map a caller-owned host range (include/leopard_amd.h)."""
+    return LeopardResult(lib.leo_amd_register_host(ctypes.c_void_p(ptr), nbytes))
+
+
+def unregister_host(ptr: int) -> LeopardResult:
+    return LeopardResult(lib.leo_amd_unregister_host(ctypes.c_void_p(ptr)))
+
+
 def set_stream(stream_handle: Optional[int]) -> None:
     """HIP stream (integer handle, e.g. torch.cuda.current_stream().cuda_stream) for this thread."""
     lib.leo_amd_set_stream(None if not stream_handle else ctypes.c_void_p(stream_handle))
@@ -174,6 +186,11 @@ def set_async(enable: bool) -> None:
 
 def set_device(device: int) -> None:
     lib.leo_amd_set_device(int(device))
+
+
+def set_fanout(ranges: int) -> None:
+    """Host-memory calls split their columns over `ranges` device workers (-1 = every device)."""
+    lib.leo_amd_set_fanout(int(ranges))
 
 
 def device_count() -> int:

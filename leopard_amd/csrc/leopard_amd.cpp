@@ -14,6 +14,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -34,6 +35,8 @@ struct ThreadState {
     hipStream_t stream = nullptr;
     bool async = false;
     int device = -1;
+    int fanout = 0;               // leo_amd_set_fanout (0 = LEO_AMD_FANOUT, default 1)
+    bool fanout_worker = false;   // this thread runs one range of a fanned-out call
     std::string last_error;
 };
 thread_local ThreadState tls;
@@ -849,6 +852,135 @@ LeopardResult run_host_pipeline(Call& c, uint64_t bytes, const std::vector<const
     return scatter(nslices - 1);
 }
 
+// ------------------------------------------------ registered host memory --
+
+// Caller-registered host memory (leo_amd_register_host): pinned and mapped
+// into every device's address space, so kernels read the caller's pieces and
+// write the results in place over PCIe -- no staging copies.  The caller keeps
+// a registered range alive until it unregisters it (the contract of
+// hipHostRegister / RDMA memory registration).
+struct HostReg {
+    uintptr_t base;
+    uint64_t size;
+    uintptr_t dbase;  // device address of base
+};
+std::mutex g_reg_mu;
+std::map<uintptr_t, HostReg> g_regs;
+
+// Device addresses of ptrs[i] + [off, off + bytes) when every non-null piece
+// lies in one registered range; else false.
+bool map_registered(const void* const* ptrs, unsigned count, uint64_t off, uint64_t bytes, std::vector<void*>& out) {
+    out.assign(count, nullptr);
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    if (g_regs.empty()) return false;
+    for (unsigned i = 0; i < count; ++i) {
+        if (!ptrs[i]) continue;
+        const uintptr_t p = reinterpret_cast<uintptr_t>(ptrs[i]);
+        auto it = g_regs.upper_bound(p);
+        if (it == g_regs.begin()) return false;
+        --it;
+        const HostReg& r = it->second;
+        if (p + off + bytes > r.base + r.size) return false;
+        out[i] = reinterpret_cast<void*>(r.dbase + (p - r.base));
+    }
+    return true;
+}
+
+// ------------------------------------------------------ multi-GPU fan-out --
+
+// A host-memory call (the reference's contract: caller-owned host buffers)
+// can split its columns over several GPUs, each staging or reading its range
+// over its own PCIe link.  Range i runs on device
+// i % device_count on fan-out worker i, a persistent thread that keeps its own
+// per-device workspaces; the call returns when every range is done.
+class FanoutPool {
+public:
+    static FanoutPool& get() {
+        static FanoutPool* pool = new FanoutPool();  // never destroyed (detached workers)
+        return *pool;
+    }
+    void run(unsigned n, const std::function<void(unsigned)>& fn) {
+        std::lock_guard<std::mutex> call(call_mu_);
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            while (workers_ < n) {
+                const unsigned id = workers_++;
+                const uint64_t seen = gen_;
+                std::thread([this, id, seen] { loop(id, seen); }).detach();
+            }
+            fn_ = &fn;
+            n_ = n;
+            pending_ = n;
+            ++gen_;
+        }
+        cv_.notify_all();
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [&] { return pending_ == 0; });
+        fn_ = nullptr;
+    }
+
+private:
+    void loop(unsigned id, uint64_t seen) {
+        for (;;) {
+            const std::function<void(unsigned)>* fn = nullptr;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return gen_ != seen; });
+                seen = gen_;
+                if (id >= n_) continue;
+                fn = fn_;
+            }
+            (*fn)(id);
+            std::lock_guard<std::mutex> lk(mu_);
+            if (--pending_ == 0) done_.notify_all();
+        }
+    }
+    std::mutex call_mu_, mu_;
+    std::condition_variable cv_, done_;
+    const std::function<void(unsigned)>* fn_ = nullptr;
+    unsigned workers_ = 0, n_ = 0, pending_ = 0;
+    uint64_t gen_ = 0;
+};
+
+// Ranges a host-memory call of `bytes` columns is split into: the thread's
+// leo_amd_set_fanout value, else LEO_AMD_FANOUT (default 1; -1 = every
+// device), at most one range per 4 KiB of columns.
+unsigned fanout_ranges(uint64_t bytes) {
+    static const int env = [] {
+        const char* e = std::getenv("LEO_AMD_FANOUT");
+        return e ? std::atoi(e) : 1;
+    }();
+    int n = tls.fanout != 0 ? tls.fanout : env;
+    if (n < 0) n = std::max(1, g_device_count);
+    const uint64_t cap = std::max<uint64_t>(1, bytes / 4096);
+    return unsigned(std::min<uint64_t>(std::max(n, 1), cap));
+}
+
+// fn(len, off) for each of n 64-byte-aligned column ranges of [0, bytes), one
+// per fan-out worker; returns the first failure (its error text moves to the
+// calling thread).
+LeopardResult fanout(unsigned n, uint64_t bytes, const std::function<LeopardResult(uint64_t, uint64_t)>& fn) {
+    const uint64_t blocks = bytes / 64;
+    std::vector<LeopardResult> res(n, Leopard_Success);
+    std::vector<std::string> err(n);
+    const int ndev = std::max(1, g_device_count);
+    FanoutPool::get().run(n, [&](unsigned i) {
+        const uint64_t b0 = blocks * i / n, b1 = blocks * (i + 1) / n;
+        tls.device = int(i % unsigned(ndev));
+        tls.stream = nullptr;
+        tls.async = false;
+        tls.fanout_worker = true;
+        res[i] = b1 > b0 ? fn((b1 - b0) * 64, b0 * 64) : Leopard_Success;
+        if (res[i] != Leopard_Success) err[i] = tls.last_error;
+    });
+    for (unsigned i = 0; i < n; ++i)
+        if (res[i] != Leopard_Success) {
+            tls.last_error = err[i];
+            return res[i];
+        }
+    return Leopard_Success;
+}
+
 LeopardResult encode_any(uint64_t bytes, uint64_t off, unsigned K, unsigned R, const void* const* orig, void** work);
 LeopardResult decode_any(uint64_t bytes, uint64_t off, unsigned K, unsigned R, const void* const* orig,
                          const void* const* rec, void** work);
@@ -906,6 +1038,20 @@ LeopardResult encode_any(uint64_t bytes, uint64_t off, unsigned K, unsigned R, c
             jobs.push_back({static_cast<uint8_t*>(work[i]) + off, static_cast<const uint8_t*>(orig[i]) + off, bytes});
         parallel_copy(jobs);
         return Leopard_Success;
+    }
+    if (!tls.fanout_worker) {  // columns over several GPUs
+        const unsigned nr = fanout_ranges(bytes);
+        if (nr > 1)
+            return fanout(nr, bytes, [&](uint64_t len, uint64_t o) { return encode_any(len, off + o, K, R, orig, work); });
+    }
+    {  // caller-registered host memory: the kernels run on it in place
+        std::vector<void*> di, dw;
+        if (map_registered(orig, K, off, bytes, di) && map_registered(work, R, off, bytes, dw)) {
+            r = R == 1 ? xor_device(c, bytes, off, const_cast<const void* const*>(di.data()), K, dw[0])
+                       : encode_device(c, bytes, off, K, R, const_cast<const void* const*>(di.data()), dw.data());
+            if (r != Leopard_Success) return r;
+            return finish(c, true);
+        }
     }
     std::vector<const uint8_t*> hin(K);
     std::vector<uint8_t*> hout(R);
@@ -981,6 +1127,33 @@ LeopardResult decode_any(uint64_t bytes, uint64_t off, unsigned K, unsigned R, c
                 jobs.push_back({static_cast<uint8_t*>(work[i]) + off, static_cast<const uint8_t*>(orig[i]) + off, bytes});
         parallel_copy(jobs);
         return Leopard_Success;
+    }
+    if (!tls.fanout_worker) {  // columns over several GPUs
+        const unsigned nr = fanout_ranges(bytes);
+        if (nr > 1)
+            return fanout(nr, bytes,
+                          [&](uint64_t len, uint64_t o) { return decode_any(len, off + o, K, R, orig, rec, work); });
+    }
+    {  // caller-registered host memory: the kernels run on it in place
+        std::vector<void*> dorig, drec, dwork;
+        std::vector<const void*> wl(K, nullptr);  // only the work pieces of lost originals are written
+        for (unsigned i = 0; i < K; ++i)
+            if (!orig[i]) wl[i] = work[i];
+        if (map_registered(orig, K, off, bytes, dorig) && map_registered(rec, R, off, bytes, drec) &&
+            map_registered(wl.data(), K, off, bytes, dwork)) {
+            if (R == 1) {  // leopard.cpp:294-303
+                std::vector<const void*> src;
+                src.push_back(drec[0]);
+                for (unsigned i = 0; i < K; ++i)
+                    if (orig[i]) src.push_back(dorig[i]);
+                r = xor_device(c, bytes, off, src.data(), unsigned(src.size()), dwork[lost_i]);
+            } else {
+                r = decode_device(c, bytes, off, K, R, const_cast<const void* const*>(dorig.data()),
+                                  const_cast<const void* const*>(drec.data()), dwork.data());
+            }
+            if (r != Leopard_Success) return r;
+            return finish(c, true);
+        }
     }
     // Slice rows: received recoveries first, then received originals (so the
     // R == 1 XOR sources form one slab), outputs = lost originals in order.
@@ -1304,9 +1477,43 @@ LEO_EXPORT LeopardResult leo_amd_decode_batch(unsigned object_count, uint64_t bu
                         recovery_data, work_data);
 }
 
+LEO_EXPORT LeopardResult leo_amd_register_host(void* ptr, uint64_t bytes) {
+    if (!ptr || bytes == 0) return Leopard_InvalidInput;
+    hipError_t e = hipHostRegister(ptr, bytes, hipHostRegisterMapped | hipHostRegisterPortable);
+    if (e != hipSuccess) {
+        set_error("hipHostRegister", e);
+        return Leopard_Platform;
+    }
+    void* d = nullptr;
+    e = hipHostGetDevicePointer(&d, ptr, 0);
+    if (e != hipSuccess) {
+        set_error("hipHostGetDevicePointer", e);
+        (void)hipHostUnregister(ptr);
+        return Leopard_Platform;
+    }
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    const uintptr_t b = reinterpret_cast<uintptr_t>(ptr);
+    g_regs[b] = HostReg{b, bytes, reinterpret_cast<uintptr_t>(d)};
+    return Leopard_Success;
+}
+
+LEO_EXPORT LeopardResult leo_amd_unregister_host(void* ptr) {
+    {
+        std::lock_guard<std::mutex> lk(g_reg_mu);
+        if (g_regs.erase(reinterpret_cast<uintptr_t>(ptr)) == 0) return Leopard_InvalidInput;
+    }
+    const hipError_t e = hipHostUnregister(ptr);
+    if (e != hipSuccess) {
+        set_error("hipHostUnregister", e);
+        return Leopard_Platform;
+    }
+    return Leopard_Success;
+}
+
 LEO_EXPORT void leo_amd_set_stream(void* hip_stream) { tls.stream = static_cast<hipStream_t>(hip_stream); }
 LEO_EXPORT void leo_amd_set_async(int async_enable) { tls.async = async_enable != 0; }
 LEO_EXPORT void leo_amd_set_device(int device) { tls.device = device; }
+LEO_EXPORT void leo_amd_set_fanout(int ranges) { tls.fanout = ranges; }
 
 LEO_EXPORT int leo_amd_device_count(void) {
     int count = 0;

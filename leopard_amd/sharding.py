@@ -69,6 +69,9 @@ def max_over_ranks(value: float, group=None) -> float:
     import torch.distributed as dist
     if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
         return float(value)
-    t = torch.tensor([float(value)], dtype=torch.float64)
+    device = "cpu"
+    if dist.get_backend(group) == dist.Backend.NCCL:  # RCCL reduces device tensors only
+        device = torch.device("cuda", torch.cuda.current_device())
+    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return float(t.item())

@@ -1,12 +1,10 @@
 """GPU sweeps modelled on the reference's own test driver (tests/benchmark.cpp):
 
-* exhaustive small codes, tests/benchmark.cpp:604-617: every K in [1, 256], every
-  R in [1, K], loss = R.  The encoder output is compared with the CPU oracle byte
-  for byte, and the decode of the benchmark's loss pattern (ShuffleDeck16,
-  tests/benchmark.cpp:440-467) must return the originals.  The full triangle is
-  32896 codes; this runs every code with K <= 64, every code of the rows K in
-  {127, 128, 129, 255, 256} (the FF8 chunking and FF8/FF16 boundaries) and every
-  13th R (plus R = K) elsewhere.
+* exhaustive small codes, tests/benchmark.cpp:603-618: every K in [1, 256] and
+  every R in [1, K] (all 32896 codes), loss = R.  The encoder output is
+  compared with the CPU oracle byte for byte, and the decode of the benchmark's
+  loss pattern (ShuffleDeck16, tests/benchmark.cpp:440-467) must return the
+  originals.  Split by K range so that every test finishes in seconds.
 * random codes, tests/benchmark.cpp:572-600: the reference driver's PCG-drawn
   (K, R, loss) for "small" (K <= 128) and "large" (K <= 32768) codes.
 
@@ -23,16 +21,6 @@ torch = pytest.importorskip("torch")
 B = 64
 
 
-def _codes():
-    for k in range(1, 257):
-        full = k <= 64 or k in (127, 128, 129, 255, 256)
-        rs = list(range(1, k + 1, 1 if full else 13))
-        if rs[-1] != k:
-            rs.append(k)
-        for r in rs:
-            yield k, r
-
-
 def _roundtrip(leo, data_d, data_np, k, r, loss, seed, trial):
     rec_d = leo.encode(data_d, r).clone()
     torch.cuda.synchronize()
@@ -40,19 +28,26 @@ def _roundtrip(leo, data_d, data_np, k, r, loss, seed, trial):
     lo, lr = ol.benchmark_losses(k, r, loss, seed=seed, trial=trial)
     got = leo.decode(data_d, rec_d, lo, lr)
     torch.cuda.synchronize()
-    for i in lo:
-        assert torch.equal(got[i], data_d[i]), (k, r, loss, i)
+    if lo:
+        idx = torch.tensor(lo, device="cuda")
+        assert torch.equal(torch.stack([got[i] for i in lo]), data_d.index_select(0, idx)), (k, r, loss)
 
 
-def test_exhaustive_small_codes(leo):
-    """tests/benchmark.cpp:604-617 (thinned, see the module doc)."""
+K_RANGES = [(1, 64), (65, 96), (97, 128), (129, 150), (151, 170), (171, 190), (191, 208), (209, 224), (225, 240),
+            (241, 256)]
+
+
+@pytest.mark.parametrize("k0,k1", K_RANGES)
+def test_exhaustive_small_codes(leo, k0, k1):
+    """tests/benchmark.cpp:603-618: every code with k0 <= K <= k1, every R <= K."""
     pool = ol.pcg_bytes(3, 0, 256, B)
     pool_d = torch.from_numpy(pool).cuda()
     n = 0
-    for k, r in _codes():
-        _roundtrip(leo, pool_d[:k], pool[:k], k, r, r, seed=3, trial=k * 1000 + r)
-        n += 1
-    assert n > 3000
+    for k in range(k0, k1 + 1):
+        for r in range(1, k + 1):
+            _roundtrip(leo, pool_d[:k], pool[:k], k, r, r, seed=3, trial=k * 1000 + r)
+            n += 1
+    assert n == sum(k for k in range(k0, k1 + 1))
 
 
 def _random_codes(max_k, count, seed):

@@ -512,8 +512,8 @@ void erasures8(unsigned K, unsigned R, unsigned m, const void* const* orig, cons
 // returns true when the half-position decoder applies (no original survives
 // and n = 2m: every received piece is in the low half of the positions, every
 // output in the high half; k_ff8_dec_half, rs_ff8.hip).
-bool fill_dec8(Ff8DecArgs& a, const DeviceTables* t, unsigned K, unsigned R, const void* const* orig,
-               const void* const* rec, void** work, uint64_t off, uint64_t bytes) {
+int fill_dec8(Ff8DecArgs& a, const DeviceTables* t, unsigned K, unsigned R, const void* const* orig,
+              const void* const* rec, void** work, uint64_t off, uint64_t bytes) {
     const unsigned m = next_pow2(R);
     const unsigned Tn = log2u(next_pow2(m + K));
     std::memset(&a, 0, sizeof(a));
@@ -559,17 +559,62 @@ bool fill_dec8(Ff8DecArgs& a, const DeviceTables* t, unsigned K, unsigned R, con
     bool any_orig = false;
     for (unsigned i = 0; i < K; ++i) any_orig |= orig[i] != nullptr;
     const bool half = !any_orig && Tn >= 2 && 2 * m == (1u << Tn) && ff8_half_decoder_enabled();
-    if (half) a.fused = t->fused8 + size_t(Tn - 2) * 256 * kTab8Dwords;  // T = Tn - 1, chunk 0
-    return half;
+    if (!half) return kDec8General;
+    a.fused = t->fused8 + size_t(Tn - 2) * 256 * kTab8Dwords;  // T = Tn - 1, chunk 0
+    bool all_rec = K == m && R == m;
+    for (unsigned i = 0; i < R && all_rec; ++i) all_rec = rec[i] != nullptr;
+    a.dense = all_rec ? 1u : 0u;
+    return all_rec ? kDec8HalfDense : kDec8Half;
+}
+
+// LEO_AMD_FF8_INVERT=0 turns the inverse full-loss decoder off (A/B); read once.
+bool ff8_invert_enabled() {
+    static const bool v = [] {
+        const char* e = std::getenv("LEO_AMD_FF8_INVERT");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
+// Full loss of a K = R = m code (every original lost, every recovery piece
+// received; the benchmark's worst case at 128+128): the decoder is the inverse
+// of the encoder's transform pair (launch_ff8_decode_full, rs_ff8.hip).
+bool full_loss_square(unsigned K, unsigned R, const void* const* orig, const void* const* rec) {
+    if (K < 2 || K != R || next_pow2(R) != R || !ff8_invert_enabled()) return false;
+    for (unsigned i = 0; i < K; ++i)
+        if (orig[i] || !rec[i]) return false;
+    return true;
+}
+void fill_dec8_full(Ff8EncArgs& a, const DeviceTables* t, unsigned m, const void* const* rec, void** work,
+                    uint64_t off, uint64_t bytes) {
+    std::memset(&a, 0, sizeof(a));
+    for (unsigned i = 0; i < m; ++i) {
+        a.ptr[i] = uint64_t(reinterpret_cast<uintptr_t>(rec[i])) + off;
+        a.ptr[m + i] = uint64_t(reinterpret_cast<uintptr_t>(work[i])) + off;
+    }
+    a.sktab = t->sktab8;
+    a.fused = t->fused8 + size_t(log2u(m) - 1) * 256 * kTab8Dwords;  // encoder chunk 0 of this m
+    a.K = a.R = m;
+    a.nchunks = 1;
+    a.nunits = uint32_t(bytes / 4);
 }
 
 LeopardResult decode_device8(Call& c, uint64_t bytes, uint64_t off, unsigned K, unsigned R, const void* const* orig,
                              const void* const* rec, void** work) {
     const unsigned Tn = log2u(next_pow2(next_pow2(R) + K));
+    if (full_loss_square(K, R, orig, rec)) {
+        Ff8EncArgs e;
+        for (uint64_t pos = 0; pos < bytes; pos += kFf8MaxLaunchBytes) {
+            fill_dec8_full(e, c.t, R, rec, work, off + pos, std::min(kFf8MaxLaunchBytes, bytes - pos));
+            HIP_OK(launch_ff8_decode_full(Tn - 1, e, c.s), "decode kernel");
+        }
+        return Leopard_Success;
+    }
     Ff8DecArgs a;
     for (uint64_t pos = 0; pos < bytes; pos += kFf8MaxLaunchBytes) {  // see encode_device
-        const bool half = fill_dec8(a, c.t, K, R, orig, rec, work, off + pos, std::min(kFf8MaxLaunchBytes, bytes - pos));
-        HIP_OK(half ? launch_ff8_decode_half(Tn - 1, a, c.s) : launch_ff8_decode(Tn, a, c.s), "decode kernel");
+        const int mode = fill_dec8(a, c.t, K, R, orig, rec, work, off + pos, std::min(kFf8MaxLaunchBytes, bytes - pos));
+        HIP_OK(mode != kDec8General ? launch_ff8_decode_half(Tn - 1, a, c.s) : launch_ff8_decode(Tn, a, c.s),
+               "decode kernel");
     }
     return Leopard_Success;
 }
@@ -1266,13 +1311,13 @@ LeopardResult run_batch8(int dev, unsigned count, Fill fill, Launch launch) {
     r = c.ws->reserve_device(bytes);
     if (r != Leopard_Success) return r;
     Args* dargs = reinterpret_cast<Args*>(c.ws->dbuf);
-    bool all_flag = true;
+    int kind = INT32_MAX;  // the least specialised kind over the objects
     r = c.ws->upload(dargs, bytes, c.s, [&](uint8_t* h) {
         Args* ha = reinterpret_cast<Args*>(h);
-        for (unsigned o = 0; o < count; ++o) all_flag &= fill(ha[o], c.t, o);
+        for (unsigned o = 0; o < count; ++o) kind = std::min(kind, fill(ha[o], c.t, o));
     });
     if (r != Leopard_Success) return r;
-    HIP_OK(launch(dargs, all_flag, c.s), "batch kernel");
+    HIP_OK(launch(dargs, kind, c.s), "batch kernel");
     return finish(c, false);
 }
 
@@ -1294,10 +1339,11 @@ LeopardResult encode_batch(unsigned count, uint64_t bytes, unsigned K, unsigned 
             dev, count,
             [&](Ff8EncArgs& a, const DeviceTables* t, unsigned o) {
                 fill_enc8(a, t, K, R, orig[o], work[o], 0, bytes);
-                return true;
+                return 0;
             },
-            [&](const Ff8EncArgs* d, bool, hipStream_t s) {
-                return launch_ff8_encode_batch(Tm, d, count, uint32_t(bytes / 4), (K + m - 1) / m > 1, s);
+            [&](const Ff8EncArgs* d, int, hipStream_t s) {
+                return launch_ff8_encode_batch(Tm, d, count, uint32_t(bytes / 4), (K + m - 1) / m > 1,
+                                               K == m && R == m ? kFormDenseEnc : kFormGeneral, s);
             });
     }
     for (unsigned o = 0; o < count; ++o) {
@@ -1338,13 +1384,26 @@ LeopardResult decode_batch(unsigned count, uint64_t bytes, unsigned K, unsigned 
         }
         if (batch_on_device(count, firsts.data(), &dev)) {
             const unsigned Tn = log2u(n);
+            bool full = true;  // every object a full loss of a K = R = m code: the inverse encoder tile
+            for (unsigned o = 0; o < count && full; ++o) full = full_loss_square(K, R, orig[o], rec[o]);
+            if (full)
+                return run_batch8<Ff8EncArgs>(
+                    dev, count,
+                    [&](Ff8EncArgs& a, const DeviceTables* t, unsigned o) {
+                        fill_dec8_full(a, t, m, rec[o], work[o], 0, bytes);
+                        return 0;
+                    },
+                    [&](const Ff8EncArgs* d, int, hipStream_t s) {
+                        return launch_ff8_encode_batch(Tn - 1, d, count, uint32_t(bytes / 4), false, kFormDenseDec, s);
+                    });
             return run_batch8<Ff8DecArgs>(
                 dev, count,
                 [&](Ff8DecArgs& a, const DeviceTables* t, unsigned o) {
                     return fill_dec8(a, t, K, R, orig[o], rec[o], work[o], 0, bytes);
                 },
-                [&](const Ff8DecArgs* d, bool half, hipStream_t s) {
-                    return launch_ff8_decode_batch(half ? Tn - 1 : Tn, d, count, uint32_t(bytes / 4), half, s);
+                [&](const Ff8DecArgs* d, int mode, hipStream_t s) {
+                    return launch_ff8_decode_batch(mode != kDec8General ? Tn - 1 : Tn, d, count, uint32_t(bytes / 4),
+                                                   mode, s);
                 });
         }
     }

@@ -69,7 +69,14 @@ struct Ff8DecArgs {
     const uint32_t* fused;         // k_ff8_dec_half: fused top-layer table of this m (= encoder chunk 0's)
     unsigned K, R, m;
     uint32_t nunits;
+    uint32_t dense;                // half decoder with K = R = m, every recovery received (host-side dispatch)
 };
+// GF(2^8) decoder kinds of one argument block (fill_dec8, launch_ff8_decode_batch)
+constexpr int kDec8General = 0, kDec8Half = 1, kDec8HalfDense = 2;
+// Forms of the GF(2^8) encoder tile (k_ff8_enc): general (pruned, chunked),
+// dense encode (one chunk, K = R = m), dense inverse (full-loss decode of a
+// K = R = m code, launch_ff8_decode_full).
+constexpr int kFormGeneral = 0, kFormDenseEnc = 1, kFormDenseDec = 2;
 
 struct XorArgs {
     PieceMap src;
@@ -96,11 +103,12 @@ hipError_t launch_ff8_encode(unsigned T, const Ff8EncArgs& a, hipStream_t s);
 hipError_t launch_ff8_decode(unsigned T, const Ff8DecArgs& a, hipStream_t s);
 // Batched GF(2^8) launches: `count` argument blocks in device memory (same T,
 // column count and chunk structure), one grid (strips x objects).  For the
-// decoder, half = every object qualifies for k_ff8_dec_half (T is then the
-// half tile's bits, as for launch_ff8_decode_half).
+// decoder, mode = the least specialised kDec8* kind over the objects (T is the
+// half tile's bits for the half kinds, as for launch_ff8_decode_half).
 hipError_t launch_ff8_encode_batch(unsigned T, const Ff8EncArgs* objs, unsigned count, uint32_t nunits, bool multi,
-                                   hipStream_t s);
-hipError_t launch_ff8_decode_batch(unsigned T, const Ff8DecArgs* objs, unsigned count, uint32_t nunits, bool half,
+                                   int form, hipStream_t s);
+hipError_t launch_ff8_decode_full(unsigned Tm, const Ff8EncArgs& a, hipStream_t s);
+hipError_t launch_ff8_decode_batch(unsigned T, const Ff8DecArgs* objs, unsigned count, uint32_t nunits, int mode,
                                    hipStream_t s);
 
 // Units per lane chosen for each kernel family (the host sizes grids with it).

@@ -298,10 +298,20 @@ struct LdsSkew8 {
     int off = 0;
     LDEV FF8::Tab table(unsigned cidx) const { return tabs.at(off + int(cidx)); }
     LDEV void stage(const uint32_t*, int o) { off = o; }
+    // The skew of position j is zero exactly at j = 2^k - 1 (FFTSkew[2^k - 1]
+    // = 0, LeopardFF8.cpp:496-538): such a butterfly is the reference's XOR-only
+    // form (its multiply-add adds 0).  Wave-uniform.  With skew base -1 (the
+    // FFT of every encode, the IFFT of every decode) this is group 0 of every
+    // layer: 63 of the 448 butterflies of a 128-point transform.
+    LDEV bool zero(unsigned cidx) const {
+        const unsigned j = unsigned(off + int(cidx));
+        return ((j + 1) & j) == 0;
+    }
 };
 template <class F>
 struct GlobalWindow {
     const uint32_t* sk = nullptr;
+    LDEV constexpr bool zero(unsigned) const { return false; }
     LDEV typename F::Tab table(unsigned cidx) const { return F::tab_at(sk + size_t(cidx) * F::kTabDw); }
     LDEV void stage(const uint32_t* sktab, int off) { sk = sktab + ptrdiff_t(off) * ptrdiff_t(F::kTabDw); }
 };
@@ -318,6 +328,7 @@ struct GlobalWindow {
 struct LdsWindow16 {
     const uint32_t* set;
     unsigned hi_fixed, l0;
+    LDEV constexpr bool zero(unsigned) const { return false; }
     LDEV FF16::Tab table(unsigned cidx) const { return FF16::tab_lds(set + ((cidx - hi_fixed) >> l0) * 20u); }
     LDEV void stage(const uint32_t*, int) {}
 };
@@ -567,9 +578,17 @@ struct Tile {
         auto live = [&](int g) { return pred(ps.global(piece(LAY, g, w)), gl + 1); };
         auto table = [&](int g) {
             // A zero skew has an all-zero table: the multiply-add adds 0, which is
-            // the reference's XOR-only butterfly without a branch (branches around
-            // register-array updates cost whole-array copies at the merge).
+            // the reference's XOR-only butterfly.
             return win.table(skew_index(ps.global(piece(LAY, g, w)), gl));
+        };
+        auto zero = [&](int g) { return win.zero(skew_index(ps.global(piece(LAY, g, w)), gl)); };
+        // XOR-only butterflies of a zero-skew group (wave-uniform branch): the
+        // IFFT's y ^= x; x ^= 0 and the FFT's x ^= 0; y ^= x are both y ^= x.
+        auto xor_group = [&](int g) {
+#pragma unroll
+            for (int j = 0; j < half; ++j)
+#pragma unroll
+                for (int k = 0; k < U; ++k) x[g + j + half][k] ^= x[g + j][k];
         };
         constexpr int NG = NR / (2 * half);  // groups (distinct skews) per lane in this layer
         auto group = [&](int g, const typename F::Tab& t) {
@@ -618,7 +637,10 @@ struct Tile {
                 static_for<0, KB>([&](auto GI) { tabs[GI.value] = table((g0 + GI.value) * 2 * half); });
                 static_for<0, KB>([&](auto GI) {
                     constexpr int g = (g0 + GI.value) * 2 * half;
-                    if (live(g)) group(g, tabs[GI.value]);
+                    if (live(g)) {
+                        if (zero(g)) xor_group(g);
+                        else group(g, tabs[GI.value]);
+                    }
                 });
                 __builtin_amdgcn_sched_barrier(0);  // keep the next batch's tables below this one
             });

@@ -158,8 +158,16 @@ LDEV auto lane_pred(const P& p) {
     else return AnyLane<P>{p};
 }
 
-template <int T, int RB, bool kMulti, int NA, int G>
+// kForm (Ff8Form): kFormDenseEnc = one chunk with K = R = m (the 128+128
+// headline shape): every block of both transforms is live and every tile piece
+// is loaded and stored, so the pruning predicates and the per-piece bounds
+// tests compile away (they were a third of the kernel's scalar instructions).
+// kFormDenseDec = the same tile run as the inverse map, the full-loss decode of
+// a K = R = m code (see launch_ff8_decode_full).
+template <int T, int RB, bool kMulti, int NA, int G, int kForm = kFormGeneral>
 LDEV void ff8_enc(const Ff8EncArgs& a) {
+    constexpr bool kDense = kForm != kFormGeneral;
+    static_assert(!(kDense && kMulti), "dense = one chunk");
     if constexpr ((LAMD_ABLATE & 16) != 0) return;
     // G lane-group bits: the wave's 64 lanes hold 2^G column strips of LW lanes
     // for different pieces (virtual wave w = lane group above the real wave), so
@@ -197,7 +205,8 @@ LDEV void ff8_enc(const Ff8EncArgs& a) {
 #pragma unroll
             for (int r = 0; r < TL::NR; ++r) {
                 const unsigned i = base + TL::piece(0, r, w);
-                x[r][0] = i < a.K ? gload(pp[r], cl) : 0u;  // past K: zero padding (LeopardFF8.cpp:1631-1634)
+                if constexpr (kDense) x[r][0] = gload(pp[r], cl);
+                else x[r][0] = i < a.K ? gload(pp[r], cl) : 0u;  // past K: zero padding (LeopardFF8.cpp:1631-1634)
             }
         } else {
             // per-lane pieces: branch-free, padding lanes re-read piece K - 1 and drop it
@@ -229,7 +238,14 @@ LDEV void ff8_enc(const Ff8EncArgs& a) {
     __syncthreads();
     STAMP(2);
     LdsSkew8 win{tabs};
-    if constexpr (!kMulti) {
+    if constexpr (kDense) {
+        // encode: IFFT skew base m - 1, FFT base -1; inverse: the other way round
+        win.stage(nullptr, kForm == kFormDenseDec ? -1 : int(m - 1));
+        ifft(win, AllLive{});
+        TL::fused_top(x, FF8::tab_at(a.fused));
+        win.stage(nullptr, kForm == kFormDenseDec ? int(m - 1) : -1);
+        fft(win, AllLive{});
+    } else if constexpr (!kMulti) {
         win.stage(nullptr, int(m - 1));
         ifft(win, lane_pred<G>(BelowLive{a.K}));
         STAMP(3);
@@ -259,21 +275,21 @@ LDEV void ff8_enc(const Ff8EncArgs& a) {
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) {
         const unsigned tp = TL::piece(0, r, w);
-        if (tp < a.R) gstore(pp[r], cl, x[r][0]);
+        if (kDense || tp < a.R) gstore(pp[r], cl, x[r][0]);
     }
     STAMP(5);
 }
 
-template <int T, int RB, bool kMulti, int NA, int G>
+template <int T, int RB, bool kMulti, int NA, int G, int kForm = kFormGeneral>
 __global__ void __launch_bounds__(threads_for(T, RB) >> G, 4) k_ff8_enc(Ff8EncArgs a) {
-    ff8_enc<T, RB, kMulti, NA, G>(a);
+    ff8_enc<T, RB, kMulti, NA, G, kForm>(a);
 }
 // Batched launch (leo_amd_encode_batch): object blockIdx.y of an array of
 // argument blocks in device memory (read through the scalar cache like the
 // kernel arguments of k_ff8_enc); one grid over every object's column strips.
-template <int T, int RB, bool kMulti>
+template <int T, int RB, bool kMulti, int kForm = kFormGeneral>
 __global__ void __launch_bounds__(threads_for(T, RB), 4) k_ff8_enc_batch(const Ff8EncArgs* __restrict__ objs) {
-    ff8_enc<T, RB, kMulti, 1, 0>(objs[blockIdx.y]);
+    ff8_enc<T, RB, kMulti, 1, 0, kForm>(objs[blockIdx.y]);
 }
 
 // --------------------------------------------------------------- decode -----
@@ -380,7 +396,10 @@ __global__ void __launch_bounds__(threads_for(T, RB), 4) k_ff8_dec_batch(const F
 // high positions (the encoder's transform pair with the halves exchanged, so
 // the top layers fuse as in the encoder), no derivative, every wave busy (in k_ff8_dec the waves of the
 // empty high half idle through the scale and the low IFFT layers).
-template <int T, int RB>
+// kDense: K = R = m and every recovery piece received (full loss of the
+// originals, the benchmark's worst case): all low positions present, all high
+// ones needed, so the pyramid predicates compile away.
+template <int T, int RB, bool kDense = false>
 LDEV void ff8_dec_half(const Ff8DecArgs& a) {
     if constexpr ((LAMD_ABLATE & 16) != 0) return;
     using F = FF8;
@@ -395,7 +414,11 @@ LDEV void ff8_dec_half(const Ff8DecArgs& a) {
     const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const Cols cl = strip_cols(a.nunits, lane);
     const PieceSpace low{0, 0, 0}, high{0, 0, m};
-    const Pyr8Live present{a.present}, needed{a.needed};
+    auto pyr = [](const uint32_t* w) {
+        if constexpr (kDense) return AllLive{};
+        else return Pyr8Live{w};
+    };
+    const auto present = pyr(a.present), needed = pyr(a.needed);
     auto lpos = [&](int r) { return TL::piece(0, r, w); };
     auto hpos = [&](int r) { return m + TL::piece(0, r, w); };
     typename TL::Reg v;
@@ -426,13 +449,13 @@ LDEV void ff8_dec_half(const Ff8DecArgs& a) {
     for (int r = 0; r < TL::NR; ++r)
         if (is_needed(r)) gstore(pp[r], cl, v[r][0]);
 }
-template <int T, int RB>
+template <int T, int RB, bool kDense>
 __global__ void __launch_bounds__(threads_for(T, RB), 4) k_ff8_dec_half(Ff8DecArgs a) {
-    ff8_dec_half<T, RB>(a);
+    ff8_dec_half<T, RB, kDense>(a);
 }
-template <int T, int RB>
+template <int T, int RB, bool kDense>
 __global__ void __launch_bounds__(threads_for(T, RB), 4) k_ff8_dec_half_batch(const Ff8DecArgs* __restrict__ objs) {
-    ff8_dec_half<T, RB>(objs[blockIdx.y]);
+    ff8_dec_half<T, RB, kDense>(objs[blockIdx.y]);
 }
 
 // Opting a kernel into > 64 KiB of LDS is a per-function attribute, set once
@@ -507,10 +530,19 @@ int enc_lane_groups(uint32_t nunits) {
     return nunits <= 16384u ? kDefaultEncG : 0;
 }
 
+// One chunk with K = R = m: the dense encoder (no pruning predicates).
+inline bool enc_dense(unsigned T, const Ff8EncArgs& a) {
+    return a.nchunks == 1 && a.K == (1u << T) && a.R == (1u << T);
+}
+
 template <int T, int RB, int NA, int G>
 hipError_t enc_RBG(const Ff8EncArgs& a, hipStream_t s) {
     constexpr size_t lds = areas8(NA) * (tile_dwords_for(T, RB) >> G) + LdsTab8<256>::kDwords;
     constexpr unsigned threads = threads_for(T, RB) >> G;
+    if constexpr (G == 0)
+        if (enc_dense(T, a))
+            return launch8<EncTag<T, RB, false, NA, 4>>(&k_ff8_enc<T, RB, false, NA, 0, kFormDenseEnc>, threads, a, lds,
+                                                         s);
     if (a.nchunks > 1)
         return launch8<EncTag<T, RB, true, NA, G>>(&k_ff8_enc<T, RB, true, NA, G>, threads, a, lds, s, 64u >> G);
     return launch8<EncTag<T, RB, false, NA, G>>(&k_ff8_enc<T, RB, false, NA, G>, threads, a, lds, s, 64u >> G);
@@ -551,7 +583,9 @@ template <int T>
 hipError_t dec_half_T(const Ff8DecArgs& a, hipStream_t s) {
     constexpr int RB = reg_bits8(T);
     constexpr size_t lds = tile_dwords_for(T, RB) + 2 * LdsTab8<256>::kDwords;
-    return launch8<DecHalfTag<T, RB>>(&k_ff8_dec_half<T, RB>, threads_for(T, RB), a, lds, s);
+    if (a.dense)
+        return launch8<DecHalfTag<T, RB + 16>>(&k_ff8_dec_half<T, RB, true>, threads_for(T, RB), a, lds, s);
+    return launch8<DecHalfTag<T, RB>>(&k_ff8_dec_half<T, RB, false>, threads_for(T, RB), a, lds, s);
 }
 
 }  // namespace
@@ -570,6 +604,37 @@ hipError_t launch_ff8_encode(unsigned T, const Ff8EncArgs& a, hipStream_t s) {
     return e;
 }
 
+// Full-loss decode of a K = R = m code: with every original lost and every
+// recovery piece received, the decoder's map is the inverse of the encoder's
+// rec = FFT_{-1}(IFFT_{m-1}(data)) -- a bijection of m pieces, so the
+// reference decoder (which returns the unique originals) computes exactly
+//   data = FFT_{m-1}(IFFT_{-1}(rec))
+// (an IFFT inverts the FFT of the same skew base and vice versa).  That is the
+// encoder's tile with the two skew bases exchanged: no error locator, no
+// scale / reveal multiplies.  `a` is an encoder block: ptr[0, m) the recovery
+// pieces, ptr[m, 2m) the outputs, fused = the encoder's chunk-0 table (the
+// fused top layer adds the same two single skews).
+hipError_t launch_ff8_decode_full(unsigned Tm, const Ff8EncArgs& a, hipStream_t s) {
+    hipError_t e = hipErrorInvalidValue;
+    static_for<1, 8>([&](auto I) {
+        constexpr int TT = decltype(I)::value;
+        if (Tm != unsigned(TT)) return;
+        constexpr int RB = wide_bits8(TT);
+        const bool wide = RB != reg_bits8(TT) && (a.nunits >= 65536 || force_wide());
+        if (wide) {
+            constexpr size_t lds = tile_dwords_for(TT, RB) + LdsTab8<256>::kDwords;
+            e = launch8<EncTag<TT, RB, false, 1, 5>>(&k_ff8_enc<TT, RB, false, 1, 0, kFormDenseDec>,
+                                                     threads_for(TT, RB), a, lds, s);
+        } else {
+            constexpr int RN = reg_bits8(TT);
+            constexpr size_t lds = tile_dwords_for(TT, RN) + LdsTab8<256>::kDwords;
+            e = launch8<EncTag<TT, RN, false, 1, 5>>(&k_ff8_enc<TT, RN, false, 1, 0, kFormDenseDec>,
+                                                     threads_for(TT, RN), a, lds, s);
+        }
+    });
+    return e;
+}
+
 hipError_t launch_ff8_decode_half(unsigned Tm, const Ff8DecArgs& a, hipStream_t s) {
     hipError_t e = hipErrorInvalidValue;
     static_for<1, 8>([&](auto I) {
@@ -579,13 +644,19 @@ hipError_t launch_ff8_decode_half(unsigned Tm, const Ff8DecArgs& a, hipStream_t 
 }
 
 hipError_t launch_ff8_encode_batch(unsigned T, const Ff8EncArgs* objs, unsigned count, uint32_t nunits, bool multi,
-                                   hipStream_t s) {
+                                   int form, hipStream_t s) {
     hipError_t e = hipErrorInvalidValue;
     static_for<1, 8>([&](auto I) {
         constexpr int TT = decltype(I)::value, RB = batch_bits8(TT);
         constexpr size_t lds = tile_dwords_for(TT, RB) + LdsTab8<256>::kDwords;
         if (T != unsigned(TT)) return;
-        if (multi)
+        if (form == kFormDenseEnc)
+            e = launch8_batch<EncBatchTag<TT + 16, false>>(&k_ff8_enc_batch<TT, RB, false, kFormDenseEnc>,
+                                                           threads_for(TT, RB), objs, count, nunits, lds, s);
+        else if (form == kFormDenseDec)
+            e = launch8_batch<EncBatchTag<TT + 32, false>>(&k_ff8_enc_batch<TT, RB, false, kFormDenseDec>,
+                                                           threads_for(TT, RB), objs, count, nunits, lds, s);
+        else if (multi)
             e = launch8_batch<EncBatchTag<TT, true>>(&k_ff8_enc_batch<TT, RB, true>, threads_for(TT, RB), objs, count,
                                                      nunits, lds, s);
         else
@@ -595,16 +666,20 @@ hipError_t launch_ff8_encode_batch(unsigned T, const Ff8EncArgs* objs, unsigned 
     return e;
 }
 
-hipError_t launch_ff8_decode_batch(unsigned T, const Ff8DecArgs* objs, unsigned count, uint32_t nunits, bool half,
+hipError_t launch_ff8_decode_batch(unsigned T, const Ff8DecArgs* objs, unsigned count, uint32_t nunits, int mode,
                                    hipStream_t s) {
     hipError_t e = hipErrorInvalidValue;
-    if (half) {
+    if (mode != kDec8General) {
         static_for<1, 8>([&](auto I) {
             constexpr int TT = decltype(I)::value, RB = batch_bits8(TT);
             constexpr size_t lds = tile_dwords_for(TT, RB) + 2 * LdsTab8<256>::kDwords;
-            if (T == unsigned(TT))
-                e = launch8_batch<DecHalfBatchTag<TT>>(&k_ff8_dec_half_batch<TT, RB>, threads_for(TT, RB), objs, count,
-                                                       nunits, lds, s);
+            if (T != unsigned(TT)) return;
+            if (mode == kDec8HalfDense)
+                e = launch8_batch<DecHalfBatchTag<TT + 16>>(&k_ff8_dec_half_batch<TT, RB, true>, threads_for(TT, RB),
+                                                            objs, count, nunits, lds, s);
+            else
+                e = launch8_batch<DecHalfBatchTag<TT>>(&k_ff8_dec_half_batch<TT, RB, false>, threads_for(TT, RB), objs,
+                                                       count, nunits, lds, s);
         });
         return e;
     }

@@ -95,6 +95,9 @@ DEC_CASES = [  # (K, R, B, originals lost)
     (90, 90, 64 * 5, 90), (3, 3, 64, 3), (33, 33, 256, 33),
     (300, 300, 128, 300), (600, 600, 64, 600), (2000, 2000, 64, 2000),  # FF16 half-position pass 2
     (1000, 200, 64, 200), (600, 300, 64, 299), (5000, 3000, 64, 3000),
+    # every original lost with K = R = m: the inverse-transform decoder (launch_ff8_decode_full),
+    # single tile (64 KiB-piece form) and the wide form (>= 256 KiB pieces)
+    (2, 2, 64, 2), (4, 4, 64 * 3, 4), (16, 16, 64 * 33, 16), (64, 64, 256, 64), (128, 128, 1 << 18, 128),
 ]
 
 

@@ -849,9 +849,9 @@ uint64_t pipe_slot_budget() {
 }
 
 // hin: host input pieces (call offset applied); hout: host output pieces.
-// two_streams: the slice work uses no shared scratch, so slots may overlap.
+// Slot j & 1 runs on its own stream with its own scratch (per-stream workspaces).
 LeopardResult run_host_pipeline(Call& c, uint64_t bytes, const std::vector<const uint8_t*>& hin,
-                                const std::vector<uint8_t*>& hout, bool two_streams, const SliceFn& fn) {
+                                const std::vector<uint8_t*>& hout, const SliceFn& fn) {
     const uint64_t nin = hin.size(), nout = hout.size(), rows = nin + nout;
     uint64_t slice = bytes;
     if (rows * bytes > pipe_slot_budget())  // >= 4 KiB slices even when that outgrows the budget
@@ -863,7 +863,6 @@ LeopardResult run_host_pipeline(Call& c, uint64_t bytes, const std::vector<const
     Workspace& ws = *c.ws;
     const unsigned nslices = unsigned((bytes + slice - 1) / slice);
     auto len_of = [&](unsigned j) { return std::min(slice, bytes - uint64_t(j) * slice); };
-    auto stream_of = [&](unsigned s) { return two_streams ? ws.pipe_stream[s] : ws.pipe_stream[0]; };
     auto scatter = [&](unsigned j) -> LeopardResult {
         const unsigned s = j & 1;
         HIP_OK(hipEventSynchronize(ws.out_done[s]), "wait slice output");
@@ -883,7 +882,8 @@ LeopardResult run_host_pipeline(Call& c, uint64_t bytes, const std::vector<const
         for (uint64_t i = 0; i < nin; ++i) jobs.push_back({pin + i * slice, hin[i] + pos, len});
         parallel_copy(jobs);
         Call cs = c;
-        cs.s = stream_of(s);
+        cs.s = ws.pipe_stream[s];
+        cs.ws = &workspace(c.dev, cs.s);  // GF(2^16) scratch must not be shared between the two streams
         HIP_OK(hipMemcpyAsync(dev, pin, in_bytes, hipMemcpyHostToDevice, cs.s), "slice upload");
         HIP_OK(hipEventRecord(ws.in_done[s], cs.s), "record upload");
         r = fn(cs, len, dev, dev + in_bytes, slice);
@@ -1089,6 +1089,16 @@ LeopardResult encode_any(uint64_t bytes, uint64_t off, unsigned K, unsigned R, c
         if (nr > 1)
             return fanout(nr, bytes, [&](uint64_t len, uint64_t o) { return encode_any(len, off + o, K, R, orig, work); });
     }
+    // Device work of one column slice staged as dense rows: inputs = the K
+    // originals, outputs = the R recovery pieces.
+    const SliceFn slice_fn = [&](Call& cs, uint64_t len, uint8_t* din, uint8_t* dout, uint64_t stride) {
+        std::vector<const void*> di(K);
+        std::vector<void*> dw(R);
+        for (unsigned i = 0; i < K; ++i) di[i] = din + i * stride;
+        for (unsigned i = 0; i < R; ++i) dw[i] = dout + i * stride;
+        if (R == 1) return xor_device(cs, len, 0, di.data(), K, dw[0]);
+        return encode_device(cs, len, 0, K, R, di.data(), dw.data());
+    };
     {  // caller-registered host memory: the kernels run on it in place
         std::vector<void*> di, dw;
         if (map_registered(orig, K, off, bytes, di) && map_registered(work, R, off, bytes, dw)) {
@@ -1102,16 +1112,7 @@ LeopardResult encode_any(uint64_t bytes, uint64_t off, unsigned K, unsigned R, c
     std::vector<uint8_t*> hout(R);
     for (unsigned i = 0; i < K; ++i) hin[i] = static_cast<const uint8_t*>(orig[i]) + off;
     for (unsigned i = 0; i < R; ++i) hout[i] = static_cast<uint8_t*>(work[i]) + off;
-    const bool ff16 = next_pow2(next_pow2(R) + K) > 256;
-    r = run_host_pipeline(c, bytes, hin, hout, R == 1 || !ff16,
-                          [&](Call& cs, uint64_t len, uint8_t* din, uint8_t* dout, uint64_t stride) {
-                              std::vector<const void*> di(K);
-                              std::vector<void*> dw(R);
-                              for (unsigned i = 0; i < K; ++i) di[i] = din + i * stride;
-                              for (unsigned i = 0; i < R; ++i) dw[i] = dout + i * stride;
-                              if (R == 1) return xor_device(cs, len, 0, di.data(), K, dw[0]);
-                              return encode_device(cs, len, 0, K, R, di.data(), dw.data());
-                          });
+    r = run_host_pipeline(c, bytes, hin, hout, slice_fn);
     if (r != Leopard_Success) return r;
     return finish(c, true);
 }
@@ -1179,6 +1180,33 @@ LeopardResult decode_any(uint64_t bytes, uint64_t off, unsigned K, unsigned R, c
             return fanout(nr, bytes,
                           [&](uint64_t len, uint64_t o) { return decode_any(len, off + o, K, R, orig, rec, work); });
     }
+    // Device work of one column slice staged as dense rows: inputs = received
+    // recoveries, then received originals (so the R == 1 XOR sources form one
+    // slab); outputs = lost originals in order.
+    std::vector<int> in_row_rec(R, -1), in_row_orig(K, -1), out_row(K, -1);
+    int nin = 0, nout = 0;
+    for (unsigned i = 0; i < R; ++i)
+        if (rec[i]) in_row_rec[i] = nin++;
+    for (unsigned i = 0; i < K; ++i) {
+        if (orig[i]) in_row_orig[i] = nin++;
+        else out_row[i] = nout++;
+    }
+    const SliceFn slice_fn = [&](Call& cs, uint64_t len, uint8_t* din, uint8_t* dout, uint64_t stride) {
+        if (R == 1) {  // leopard.cpp:294-303
+            std::vector<const void*> src;
+            for (int j = 0; j < nin; ++j) src.push_back(din + j * stride);
+            return xor_device(cs, len, 0, src.data(), unsigned(src.size()), dout);
+        }
+        std::vector<const void*> dorig(K, nullptr), drec(R, nullptr);
+        std::vector<void*> dwork(K, nullptr);
+        for (unsigned i = 0; i < R; ++i)
+            if (in_row_rec[i] >= 0) drec[i] = din + in_row_rec[i] * stride;
+        for (unsigned i = 0; i < K; ++i) {
+            if (in_row_orig[i] >= 0) dorig[i] = din + in_row_orig[i] * stride;
+            else dwork[i] = dout + out_row[i] * stride;
+        }
+        return decode_device(cs, len, 0, K, R, dorig.data(), drec.data(), dwork.data());
+    };
     {  // caller-registered host memory: the kernels run on it in place
         std::vector<void*> dorig, drec, dwork;
         std::vector<const void*> wl(K, nullptr);  // only the work pieces of lost originals are written
@@ -1200,43 +1228,15 @@ LeopardResult decode_any(uint64_t bytes, uint64_t off, unsigned K, unsigned R, c
             return finish(c, true);
         }
     }
-    // Slice rows: received recoveries first, then received originals (so the
-    // R == 1 XOR sources form one slab), outputs = lost originals in order.
     std::vector<const uint8_t*> hin;
     std::vector<uint8_t*> hout;
-    std::vector<int> in_row_rec(R, -1), in_row_orig(K, -1), out_row(K, -1);
     for (unsigned i = 0; i < R; ++i)
-        if (rec[i]) {
-            in_row_rec[i] = int(hin.size());
-            hin.push_back(static_cast<const uint8_t*>(rec[i]) + off);
-        }
+        if (rec[i]) hin.push_back(static_cast<const uint8_t*>(rec[i]) + off);
     for (unsigned i = 0; i < K; ++i) {
-        if (orig[i]) {
-            in_row_orig[i] = int(hin.size());
-            hin.push_back(static_cast<const uint8_t*>(orig[i]) + off);
-        } else {
-            out_row[i] = int(hout.size());
-            hout.push_back(static_cast<uint8_t*>(work[i]) + off);
-        }
+        if (orig[i]) hin.push_back(static_cast<const uint8_t*>(orig[i]) + off);
+        else hout.push_back(static_cast<uint8_t*>(work[i]) + off);
     }
-    const bool ff16 = next_pow2(next_pow2(R) + K) > 256;
-    r = run_host_pipeline(c, bytes, hin, hout, R == 1 || !ff16,
-                          [&](Call& cs, uint64_t len, uint8_t* din, uint8_t* dout, uint64_t stride) {
-                              if (R == 1) {  // leopard.cpp:294-303
-                                  std::vector<const void*> src;
-                                  for (size_t j = 0; j < hin.size(); ++j) src.push_back(din + j * stride);
-                                  return xor_device(cs, len, 0, src.data(), unsigned(src.size()), dout);
-                              }
-                              std::vector<const void*> dorig(K, nullptr), drec(R, nullptr);
-                              std::vector<void*> dwork(K, nullptr);
-                              for (unsigned i = 0; i < R; ++i)
-                                  if (in_row_rec[i] >= 0) drec[i] = din + in_row_rec[i] * stride;
-                              for (unsigned i = 0; i < K; ++i) {
-                                  if (in_row_orig[i] >= 0) dorig[i] = din + in_row_orig[i] * stride;
-                                  else dwork[i] = dout + out_row[i] * stride;
-                              }
-                              return decode_device(cs, len, 0, K, R, dorig.data(), drec.data(), dwork.data());
-                          });
+    r = run_host_pipeline(c, bytes, hin, hout, slice_fn);
     if (r != Leopard_Success) return r;
     return finish(c, true);
 }

@@ -446,9 +446,14 @@ __global__ void __launch_bounds__(threads16(T, R), 4) k_dec_hi(DecArgs a) {
     TL::template ifft<true>(v, w, lane, lds, ps, win, prune16(Pyr16Live{a.present_pyr}));
     TL::derivative_swaptop(v, w, lane, lds, true);
     TL::template fft<true>(v, w, lane, lds, ps, win, prune16(Pyr16Live{a.needed_pyr}));
+    // pass 3 reads A only in low tiles holding a lost original: store nothing else
+    const Pyr16Live needed{a.needed_pyr};
     if (live)
 #pragma unroll
-        for (int r = 0; r < TL::NR; ++r) st16(a.a_out.ptr(ps.global(TL::piece(0, r, w))) + cl.strip, cl.off, v[r]);
+        for (int r = 0; r < TL::NR; ++r) {
+            const unsigned p = ps.global(TL::piece(0, r, w));
+            if (needed(p, kLoBits)) st16(a.a_out.ptr(p) + cl.strip, cl.off, v[r]);
+        }
 }
 
 // pass 2 when every received piece is in the low half (K = R, every original
@@ -686,6 +691,7 @@ template <int T>
 using EncHiMulti = EncHiFn<T, true>;
 
 constexpr int kLoR = reg16(kLoBits), kLoS = split16(kLoBits);
+constexpr unsigned kNarrowGrid = 256;  // workgroups: one per CU of an MI355X
 
 }  // namespace
 
@@ -707,8 +713,15 @@ hipError_t launch_encode_hi(const EncArgs& a, hipStream_t s) {
 }
 hipError_t launch_encode_fin(const EncArgs& a, hipStream_t s) {
     const unsigned tiles = (a.R + (1u << kLoBits) - 1) >> kLoBits;
-    return launch(&k_enc_fin<kLoR, kLoS>, dim3(tiles_for(a.nunits), tiles), threads16(kLoBits, kLoR),
-                  lds16_dwords<kLoBits, kLoR, kLoS>(1, 0), s, &a);
+    const dim3 grid(tiles_for(a.nunits), tiles);
+    // A grid of at most one workgroup per CU (e.g. R <= 256 on 64 KiB pieces):
+    // 16 pieces per lane in 16 waves (the whole 128 KiB exchange area, one
+    // workgroup per CU) halve every wave's work where the 32-piece form would
+    // leave 3 of 4 wave slots of each SIMD empty.
+    if (grid.x * grid.y <= kNarrowGrid)
+        return launch(&k_enc_fin<4, 0>, grid, threads16(kLoBits, 4), lds16_dwords<kLoBits, 4, 0>(1, 0), s, &a);
+    return launch(&k_enc_fin<kLoR, kLoS>, grid, threads16(kLoBits, kLoR), lds16_dwords<kLoBits, kLoR, kLoS>(1, 0), s,
+                  &a);
 }
 hipError_t launch_decode_lo(const DecArgs& a, hipStream_t s) {
     return launch(&k_dec_lo<kLoR, kLoS>, dim3(tiles_for(a.nunits), a.nlo), threads16(kLoBits, kLoR),

@@ -555,11 +555,13 @@ def test_batch_full_loss_and_validation(leo):
 
 
 @pytest.mark.parametrize("k,r,b,loss", [(128, 128, 1 << 16, 128), (100, 30, 64 * 1000, 17), (1000, 200, 1 << 13, 200),
-                                        (9, 1, 1 << 14, 1), (128, 128, 1 << 16, 40)])
+                                        (9, 1, 1 << 14, 1), (128, 128, 1 << 16, 40), (300, 100, 1 << 15, 10),
+                                        (1000, 200, 1 << 14, 200), (40, 10, 1 << 12, 5), (64, 1, 1 << 15, 1)])
 def test_registered_host_memory_in_place(leo, k, r, b, loss):
     """leo_amd_register_host: host pieces in registered ranges are coded in place
     by the kernels (over PCIe, no staging); results equal the oracle and the
-    decode rebuilds the originals.  Unregistering falls back to staging."""
+    decode rebuilds the originals, for one-slab and fragmented piece layouts,
+    both fields and R = 1.  Unregistering falls back to staging."""
     data = ol.pcg_bytes(8, k, k, b)
     wc, dwc = leo.leo_encode_work_count(k, r), leo.leo_decode_work_count(k, r)
     work = np.zeros((wc, b), dtype=np.uint8)

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
+#include <cstring>
 
 #define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
 
@@ -60,5 +62,41 @@ int main() {
         hipLaunchKernelGGL(copy_k, dim3(1024), dim3(256), 0, s1, (const uint4*)dh_in, (uint4*)d_a, n);
         (void)hipMemcpyAsync(h_out, d_b, bytes, hipMemcpyDeviceToHost, s2);
     });
+    // 2-D copies of column slices (128 pieces x 16 KiB of 64 KiB rows) from
+    // hipHostRegister'ed malloc memory: the staging-free host pipeline's copies.
+    {
+        const size_t rows = 128, pitch = 65536, width = 16384;
+        void* hreg = malloc(rows * pitch);
+        void* hreg2 = malloc(rows * pitch);
+        memset(hreg, 1, rows * pitch);
+        memset(hreg2, 2, rows * pitch);
+        CHECK(hipHostRegister(hreg, rows * pitch, hipHostRegisterMapped));
+        CHECK(hipHostRegister(hreg2, rows * pitch, hipHostRegisterMapped));
+        void *dreg, *dreg2;
+        CHECK(hipHostGetDevicePointer(&dreg, hreg, 0));
+        CHECK(hipHostGetDevicePointer(&dreg2, hreg2, 0));
+        const size_t n8 = rows * pitch / 16;
+        timeit("kernel reads registered malloc 8 MiB", double(rows * pitch), [&] {
+            hipLaunchKernelGGL(copy_k, dim3(512), dim3(256), 0, s1, (const uint4*)dreg, (uint4*)d_a, n8); });
+        timeit("kernel writes registered malloc 8 MiB", double(rows * pitch), [&] {
+            hipLaunchKernelGGL(copy_k, dim3(512), dim3(256), 0, s1, (const uint4*)d_b, (uint4*)dreg2, n8); });
+        timeit("kernel read + write registered, 2 streams (sum)", 2.0 * rows * pitch, [&] {
+            hipLaunchKernelGGL(copy_k, dim3(512), dim3(256), 0, s1, (const uint4*)dreg, (uint4*)d_a, n8);
+            hipLaunchKernelGGL(copy_k, dim3(512), dim3(256), 0, s2, (const uint4*)d_b, (uint4*)dreg2, n8); });
+        timeit("2D H2D 128 x 16 KiB (registered)", double(rows * width), [&] {
+            (void)hipMemcpy2DAsync(d_a, width, hreg, pitch, width, rows, hipMemcpyHostToDevice, s1); });
+        timeit("2D D2H 128 x 16 KiB (registered)", double(rows * width), [&] {
+            (void)hipMemcpy2DAsync(hreg2, pitch, d_b, width, width, rows, hipMemcpyDeviceToHost, s1); });
+        timeit("2D H2D + D2H concurrently (sum)", 2.0 * rows * width, [&] {
+            (void)hipMemcpy2DAsync(d_a, width, hreg, pitch, width, rows, hipMemcpyHostToDevice, s1);
+            (void)hipMemcpy2DAsync(hreg2, pitch, d_b, width, width, rows, hipMemcpyDeviceToHost, s2); });
+        timeit("2D H2D 128 x 64 KiB whole rows (registered)", double(rows * pitch), [&] {
+            (void)hipMemcpy2DAsync(d_a, pitch, hreg, pitch, pitch, rows, hipMemcpyHostToDevice, s1); });
+        timeit("linear H2D 8 MiB (registered)", double(rows * pitch), [&] {
+            (void)hipMemcpyAsync(d_a, hreg, rows * pitch, hipMemcpyHostToDevice, s1); });
+        timeit("per-row H2D 128 x 16 KiB (registered)", double(rows * width), [&] {
+            for (size_t r = 0; r < rows; ++r)
+                (void)hipMemcpyAsync((char*)d_a + r * width, (char*)hreg + r * pitch, width, hipMemcpyHostToDevice, s1); });
+    }
     return 0;
 }

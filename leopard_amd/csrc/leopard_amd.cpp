@@ -1301,6 +1301,56 @@ bool batch_on_device(unsigned count, const void* const* firsts, int* dev) {
     return true;
 }
 
+// Pieces p[0, n) equally spaced (a slab): base and stride (two's complement).
+bool slab_of(const void* const* p, unsigned n, uint64_t& base, uint64_t& stride) {
+    base = uint64_t(reinterpret_cast<uintptr_t>(p[0]));
+    stride = n > 1 ? uint64_t(reinterpret_cast<uintptr_t>(p[1])) - base : 0;
+    for (unsigned i = 0; i < n; ++i)
+        if (!p[i] || uint64_t(reinterpret_cast<uintptr_t>(p[i])) != base + uint64_t(i) * stride) return false;
+    return true;
+}
+
+// Batch of objects whose `nin` inputs and `nout` outputs are slabs: launches
+// of up to kSlabObjs objects with every argument by value (no upload in front
+// of the kernel).  Returns false (nothing launched) when some object is not
+// slab-laid.
+bool run_slab_batch8(int dev, unsigned count, uint64_t bytes, unsigned T, unsigned K, unsigned R, unsigned nin,
+                     unsigned nout, const void* const* const* ins, void* const* const* outs, bool multi, int form,
+                     LeopardResult* res) {
+    std::vector<uint64_t> ib(count), is(count), ob(count), os(count);
+    for (unsigned o = 0; o < count; ++o)
+        if (!slab_of(ins[o], nin, ib[o], is[o]) ||
+            !slab_of(const_cast<const void* const*>(outs[o]), nout, ob[o], os[o]))
+            return false;
+    *res = [&]() -> LeopardResult {
+        DeviceGuard guard(dev);
+        Call c;
+        LeopardResult r = begin_call(dev, c);
+        if (r != Leopard_Success) return r;
+        const unsigned m = next_pow2(R);
+        Ff8SlabBatch b;
+        std::memset(&b, 0, sizeof(b));
+        b.sktab = c.t->sktab8;
+        b.fused = c.t->fused8 + size_t(T - 1) * 256 * kTab8Dwords;
+        b.K = K;
+        b.R = R;
+        b.nchunks = (K + m - 1) / m;
+        b.nunits = uint32_t(bytes / 4);
+        for (unsigned o0 = 0; o0 < count; o0 += kSlabObjs) {
+            const unsigned n = std::min(kSlabObjs, count - o0);
+            for (unsigned j = 0; j < n; ++j) {
+                b.in_base[j] = ib[o0 + j];
+                b.in_stride[j] = is[o0 + j];
+                b.out_base[j] = ob[o0 + j];
+                b.out_stride[j] = os[o0 + j];
+            }
+            HIP_OK(launch_ff8_encode_slab(T, b, n, multi, form, c.s), "slab batch kernel");
+        }
+        return finish(c, false);
+    }();
+    return true;
+}
+
 template <class Args, class Fill, class Launch>
 LeopardResult run_batch8(int dev, unsigned count, Fill fill, Launch launch) {
     DeviceGuard guard(dev);
@@ -1335,6 +1385,10 @@ LeopardResult encode_batch(unsigned count, uint64_t bytes, unsigned K, unsigned 
     int dev = -1;
     if (K > 1 && R > 1 && n <= 256 && bytes <= kFf8MaxLaunchBytes && batch_on_device(count, firsts.data(), &dev)) {
         const unsigned Tm = log2u(m);
+        const bool multi = (K + m - 1) / m > 1;
+        const int form = K == m && R == m ? kFormDenseEnc : kFormGeneral;
+        LeopardResult res;
+        if (run_slab_batch8(dev, count, bytes, Tm, K, R, K, R, orig, work, multi, form, &res)) return res;
         return run_batch8<Ff8EncArgs>(
             dev, count,
             [&](Ff8EncArgs& a, const DeviceTables* t, unsigned o) {
@@ -1386,6 +1440,9 @@ LeopardResult decode_batch(unsigned count, uint64_t bytes, unsigned K, unsigned 
             const unsigned Tn = log2u(n);
             bool full = true;  // every object a full loss of a K = R = m code: the inverse encoder tile
             for (unsigned o = 0; o < count && full; ++o) full = full_loss_square(K, R, orig[o], rec[o]);
+            LeopardResult res;
+            if (full && run_slab_batch8(dev, count, bytes, Tn - 1, m, m, m, m, rec, work, false, kFormDenseDec, &res))
+                return res;
             if (full)
                 return run_batch8<Ff8EncArgs>(
                     dev, count,

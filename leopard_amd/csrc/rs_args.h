@@ -58,6 +58,34 @@ struct Ff8EncArgs {
     const uint32_t* fused;   // fused top-layer tables of this m, entry c for chunk c (8 dwords)
     unsigned K, R, nchunks;
     uint32_t nunits;         // dword columns per piece in this launch
+    __host__ __device__ uint64_t piece(unsigned i) const { return ptr[i]; }
+};
+// Batches whose objects keep their pieces in slabs (piece i at base + i *
+// stride, the usual layout of a caller's buffer): the whole batch travels by
+// value in the kernel arguments -- no argument upload in front of the launch.
+// Encoder tile view (Ff8SlabView): pieces [0, K) = in slab, [K, K + R) = out slab.
+constexpr unsigned kSlabObjs = 64;
+struct Ff8SlabBatch {
+    uint64_t in_base[kSlabObjs], in_stride[kSlabObjs];    // column base of the launch applied
+    uint64_t out_base[kSlabObjs], out_stride[kSlabObjs];
+    const uint32_t* sktab;
+    const uint32_t* fused;
+    unsigned K, R, nchunks;
+    uint32_t nunits;
+};
+// One object of a slab batch with the interface of Ff8EncArgs (rs_ff8.hip: ff8_enc).
+struct Ff8SlabView {
+    uint64_t in_base, in_stride, out_base, out_stride;
+    const uint32_t* sktab;
+    const uint32_t* fused;
+    unsigned K, R, nchunks;
+    uint32_t nunits;
+    __host__ __device__ Ff8SlabView(const Ff8SlabBatch& b, unsigned o)
+        : in_base(b.in_base[o]), in_stride(b.in_stride[o]), out_base(b.out_base[o]), out_stride(b.out_stride[o]),
+          sktab(b.sktab), fused(b.fused), K(b.K), R(b.R), nchunks(b.nchunks), nunits(b.nunits) {}
+    __host__ __device__ uint64_t piece(unsigned i) const {
+        return i < K ? in_base + uint64_t(i) * in_stride : out_base + uint64_t(i - K) * out_stride;
+    }
 };
 struct Ff8DecArgs {
     uint64_t ptr[kFf8Ptrs];        // position p: received piece / output of a lost original / 0
@@ -70,6 +98,7 @@ struct Ff8DecArgs {
     unsigned K, R, m;
     uint32_t nunits;
     uint32_t dense;                // half decoder with K = R = m, every recovery received (host-side dispatch)
+    __host__ __device__ uint64_t piece(unsigned i) const { return ptr[i]; }
 };
 // GF(2^8) decoder kinds of one argument block (fill_dec8, launch_ff8_decode_batch)
 constexpr int kDec8General = 0, kDec8Half = 1, kDec8HalfDense = 2;
@@ -108,6 +137,11 @@ hipError_t launch_ff8_decode(unsigned T, const Ff8DecArgs& a, hipStream_t s);
 hipError_t launch_ff8_encode_batch(unsigned T, const Ff8EncArgs* objs, unsigned count, uint32_t nunits, bool multi,
                                    int form, hipStream_t s);
 hipError_t launch_ff8_decode_full(unsigned Tm, const Ff8EncArgs& a, hipStream_t s);
+// Slab batches (count <= kSlabObjs objects, arguments by value): the encoder
+// tile (form as launch_ff8_encode_batch; kFormDenseDec = full-loss decodes of
+// K = R = m codes, in = received recovery slab, out = outputs).
+hipError_t launch_ff8_encode_slab(unsigned T, const Ff8SlabBatch& b, unsigned count, bool multi, int form,
+                                  hipStream_t s);
 hipError_t launch_ff8_decode_batch(unsigned T, const Ff8DecArgs* objs, unsigned count, uint32_t nunits, int mode,
                                    hipStream_t s);
 

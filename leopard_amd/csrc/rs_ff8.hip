@@ -98,10 +98,10 @@ constexpr int kDefaultEncG = LAMD_FF8_ENC_G;
 // Piece pointers of the NR pieces a lane holds, fetched as one batch of scalar
 // loads: otherwise the compiler sinks each load into the branch that uses it,
 // a chain of dependent scalar-load round trips before the piece loads issue.
-template <int NR, class Idx>
-LDEV void fetch_ptrs(uint64_t (&pp)[NR], const uint64_t* ptr, Idx idx) {
+template <int NR, class A, class Idx>
+LDEV void fetch_ptrs(uint64_t (&pp)[NR], const A& a, Idx idx) {
 #pragma unroll
-    for (int r = 0; r < NR; ++r) pp[r] = ptr[idx(r)];
+    for (int r = 0; r < NR; ++r) pp[r] = a.piece(idx(r));
 #pragma unroll
     for (int r = 0; r < NR; ++r) asm volatile("" : "+s"(pp[r]));
 }
@@ -164,8 +164,8 @@ LDEV auto lane_pred(const P& p) {
 // tests compile away (they were a third of the kernel's scalar instructions).
 // kFormDenseDec = the same tile run as the inverse map, the full-loss decode of
 // a K = R = m code (see launch_ff8_decode_full).
-template <int T, int RB, bool kMulti, int NA, int G, int kForm = kFormGeneral>
-LDEV void ff8_enc(const Ff8EncArgs& a) {
+template <int T, int RB, bool kMulti, int NA, int G, int kForm = kFormGeneral, class A = Ff8EncArgs>
+LDEV void ff8_enc(const A& a) {
     constexpr bool kDense = kForm != kFormGeneral;
     static_assert(!(kDense && kMulti), "dense = one chunk");
     if constexpr ((LAMD_ABLATE & 16) != 0) return;
@@ -191,10 +191,10 @@ LDEV void ff8_enc(const Ff8EncArgs& a) {
     const PieceSpace ps{0, 0, 0};
     typename TL::Reg x;
     auto ptrs = [&](uint64_t (&pp)[TL::NR], auto idx) {
-        if constexpr (G == 0) fetch_ptrs(pp, a.ptr, idx);
+        if constexpr (G == 0) fetch_ptrs(pp, a, idx);
         else {
 #pragma unroll
-            for (int r = 0; r < TL::NR; ++r) pp[r] = a.ptr[idx(r)];  // per lane group
+            for (int r = 0; r < TL::NR; ++r) pp[r] = a.piece(idx(r));  // per lane group
         }
     };
     auto load_chunk = [&](unsigned c) {
@@ -292,6 +292,13 @@ __global__ void __launch_bounds__(threads_for(T, RB), 4) k_ff8_enc_batch(const F
     ff8_enc<T, RB, kMulti, 1, 0, kForm>(objs[blockIdx.y]);
 }
 
+// Slab batch (leo_amd_encode_batch / decode_batch on slab-laid objects): the
+// argument block of every object is in the kernel arguments, object blockIdx.y.
+template <int T, int RB, bool kMulti, int kForm = kFormGeneral>
+__global__ void __launch_bounds__(threads_for(T, RB), 4) k_ff8_enc_slab(Ff8SlabBatch b) {
+    ff8_enc<T, RB, kMulti, 1, 0, kForm>(Ff8SlabView(b, blockIdx.y));
+}
+
 // --------------------------------------------------------------- decode -----
 
 LDEV unsigned el_at(const Ff8DecArgs& a, unsigned p) { return (a.el[p >> 2] >> ((p & 3) * 8)) & 0xFFu; }
@@ -335,7 +342,7 @@ LDEV void ff8_dec(const Ff8DecArgs& a) {
     {
         // received pieces: positions [0, R) recovery, [m, m + K) originals (LeopardFF8.cpp:1857-1877)
         uint64_t pp[TL::NR];
-        fetch_ptrs(pp, a.ptr, pos);
+        fetch_ptrs(pp, a, pos);
 #pragma unroll
         for (int r = 0; r < TL::NR; ++r) v[r][0] = present(pos(r), 0) ? gload(pp[r], cl) : 0u;
     }
@@ -367,7 +374,7 @@ LDEV void ff8_dec(const Ff8DecArgs& a) {
     TL::pin(v);
     // lost original at p = m + i: work[i] = z[p] * exp(-el[p])  (LeopardFF8.cpp:1913-1915)
     uint64_t pp[TL::NR];
-    fetch_ptrs(pp, a.ptr, pos);
+    fetch_ptrs(pp, a, pos);
     auto is_needed = [&](int r) { return needed(pos(r), 0); };
     scale_batched<TL>(v, ltab, [&](int r) { return F::kModulus - el_at(a, pos(r)); }, is_needed);
     if (!cl.live) return;
@@ -424,7 +431,7 @@ LDEV void ff8_dec_half(const Ff8DecArgs& a) {
     typename TL::Reg v;
     {
         uint64_t pp[TL::NR];
-        fetch_ptrs(pp, a.ptr, lpos);
+        fetch_ptrs(pp, a, lpos);
 #pragma unroll
         for (int r = 0; r < TL::NR; ++r) v[r][0] = present(lpos(r), 0) ? gload(pp[r], cl) : 0u;
     }
@@ -441,7 +448,7 @@ LDEV void ff8_dec_half(const Ff8DecArgs& a) {
     TL::template fft<true>(v, w, lane, lds, high, win, needed);
     TL::pin(v);
     uint64_t pp[TL::NR];
-    fetch_ptrs(pp, a.ptr, hpos);
+    fetch_ptrs(pp, a, hpos);
     auto is_needed = [&](int r) { return needed(hpos(r), 0); };
     scale_batched<TL>(v, ltab, [&](int r) { return F::kModulus - el_at(a, hpos(r)); }, is_needed);
     if (!cl.live) return;
@@ -662,6 +669,24 @@ hipError_t launch_ff8_encode_batch(unsigned T, const Ff8EncArgs* objs, unsigned 
         else
             e = launch8_batch<EncBatchTag<TT, false>>(&k_ff8_enc_batch<TT, RB, false>, threads_for(TT, RB), objs,
                                                       count, nunits, lds, s);
+    });
+    return e;
+}
+
+hipError_t launch_ff8_encode_slab(unsigned T, const Ff8SlabBatch& b, unsigned count, bool multi, int form,
+                                  hipStream_t s) {
+    hipError_t e = hipErrorInvalidValue;
+    static_for<1, 8>([&](auto I) {
+        constexpr int TT = decltype(I)::value, RB = batch_bits8(TT);
+        constexpr size_t lds = (tile_dwords_for(TT, RB) + LdsTab8<256>::kDwords) * 4;
+        if (T != unsigned(TT)) return;
+        const void* fn = form == kFormDenseEnc   ? reinterpret_cast<const void*>(&k_ff8_enc_slab<TT, RB, false, kFormDenseEnc>)
+                         : form == kFormDenseDec ? reinterpret_cast<const void*>(&k_ff8_enc_slab<TT, RB, false, kFormDenseDec>)
+                         : multi                 ? reinterpret_cast<const void*>(&k_ff8_enc_slab<TT, RB, true>)
+                                                 : reinterpret_cast<const void*>(&k_ff8_enc_slab<TT, RB, false>);
+        static_assert(lds <= 65536, "slab batch tiles fit the default LDS limit");
+        void* params[] = {const_cast<Ff8SlabBatch*>(&b)};
+        e = hipLaunchKernel(fn, dim3((b.nunits + 63) / 64, count), dim3(threads_for(TT, RB)), params, lds, s);
     });
     return e;
 }

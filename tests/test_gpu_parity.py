@@ -484,18 +484,32 @@ def _batch_objects(k, r, b, count, seed):
     return [rng.integers(0, 256, (k, b), dtype=np.uint8) for _ in range(count)]
 
 
-@pytest.mark.parametrize("k,r,b", [(128, 128, 4096), (100, 20, 64 * 37), (200, 55, 1024), (1000, 200, 256)])
-def test_batch_encode_decode_match_oracle(leo, k, r, b):
+@pytest.mark.parametrize("k,r,b,layout", [(128, 128, 4096, "slab"), (128, 128, 4096, "shuffled"),
+                                          (100, 20, 64 * 37, "slab"), (100, 20, 64 * 37, "shuffled"),
+                                          (200, 55, 1024, "slab"), (1000, 200, 256, "slab"), (16, 16, 256, "slab")])
+def test_batch_encode_decode_match_oracle(leo, k, r, b, layout):
     """leo_amd_encode_batch / decode_batch (one launch over every object for
     GF(2^8); object by object otherwise) == independent calls == the oracle.
-    The decode batch mixes erasure patterns: full loss (half-position
-    decoder), partial losses, and objects with lost recovery pieces."""
-    count = 5
+    Slab-laid objects travel in the kernel arguments (launches of <= 64
+    objects: 16+16 runs 70 objects), shuffled piece orders through the
+    uploaded argument blocks.  The decode batch mixes erasure patterns: full
+    loss (half-position decoder), partial losses, and objects with lost
+    recovery pieces."""
+    count = 70 if k == 16 else 5
     objs = _batch_objects(k, r, b, count, k + r)
-    dev = [dev_tensor(d) for d in objs]
     wc, dwc = leo.leo_encode_work_count(k, r), leo.leo_decode_work_count(k, r)
+    if layout == "slab":
+        dev = [dev_tensor(d) for d in objs]
+        rows = [list(range(k))] * count
+    else:  # piece i of object o lives in row rows[o][i] of its tensor
+        rows = [np.random.default_rng(o).permutation(k).tolist() for o in range(count)]
+        dev = []
+        for d, rw in zip(objs, rows):
+            t = torch.empty((k, b), dtype=torch.uint8, device="cuda")
+            t[torch.tensor(rw, device="cuda")] = dev_tensor(d)
+            dev.append(t)
     works = [torch.zeros((wc, b), dtype=torch.uint8, device="cuda") for _ in range(count)]
-    res = leo.leo_amd_encode_batch(b, k, r, wc, [[t[i].data_ptr() for i in range(k)] for t in dev],
+    res = leo.leo_amd_encode_batch(b, k, r, wc, [[t[rw[i]].data_ptr() for i in range(k)] for t, rw in zip(dev, rows)],
                                    [[w[i].data_ptr() for i in range(wc)] for w in works])
     assert res == leo.LeopardResult.Success, leo.last_error()
     torch.cuda.synchronize()
@@ -512,7 +526,8 @@ def test_batch_encode_decode_match_oracle(leo, k, r, b):
     dworks = [torch.zeros((dwc, b), dtype=torch.uint8, device="cuda") for _ in range(count)]
     recd = [dev_tensor(x) for x in recs]
     res = leo.leo_amd_decode_batch(
-        b, k, r, dwc, [[None if i in lo else dev[o][i].data_ptr() for i in range(k)] for o, (lo, _) in enumerate(pats)],
+        b, k, r, dwc,
+        [[None if i in lo else dev[o][rows[o][i]].data_ptr() for i in range(k)] for o, (lo, _) in enumerate(pats)],
         [[None if i in lr else recd[o][i].data_ptr() for i in range(r)] for o, (_, lr) in enumerate(pats)],
         [[w[i].data_ptr() for i in range(dwc)] for w in dworks])
     assert res == leo.LeopardResult.Success, leo.last_error()

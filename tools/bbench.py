@@ -50,8 +50,8 @@ def main():
             dec(g)
         torch.cuda.synchronize()
         for g in range(2):
-            for i in groups[g][5]:
-                assert torch.equal(sets.dec_work[i][:k], sets.orig[i]), "decode mismatch"
+            for i in groups[g][5]:  # BB_NOCHECK=1: ablation builds (wrong results by design)
+                assert os.environ.get("BB_NOCHECK") or torch.equal(sets.dec_work[i][:k], sets.orig[i]), "decode mismatch"
 
         def t(fn, n=20):
             for j in range(4):

@@ -496,6 +496,15 @@ bool ff8_half_decoder_enabled() {
     return v;
 }
 
+// LEO_AMD_FF8_SPLIT=0 turns the split partial-loss decoder off (A/B); read once.
+bool ff8_split_decoder_enabled() {
+    static const bool v = [] {
+        const char* e = std::getenv("LEO_AMD_FF8_SPLIT");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
 // GF(2^8) erasure bitmap over 256 positions: error_locations[] = 1 at lost
 // recoveries, [R, m) and lost originals (LeopardFF8.cpp:1825-1840).
 void erasures8(unsigned K, unsigned R, unsigned m, const void* const* orig, const void* const* rec, uint32_t* erased) {
@@ -509,9 +518,10 @@ void erasures8(unsigned K, unsigned R, unsigned m, const void* const* orig, cons
 }
 
 // GF(2^8) decoder argument block of one object (columns [off, off + bytes));
-// returns true when the half-position decoder applies (no original survives
-// and n = 2m: every received piece is in the low half of the positions, every
-// output in the high half; k_ff8_dec_half, rs_ff8.hip).
+// returns the decoder kind (kDec8*): with n = 2m, the half-position decoder
+// when no original survives (every received piece in the low half of the
+// positions, every output in the high half; k_ff8_dec_half), the split decoder
+// when some do (k_ff8_dec_split); otherwise the general n-point decoder.
 int fill_dec8(Ff8DecArgs& a, const DeviceTables* t, unsigned K, unsigned R, const void* const* orig,
               const void* const* rec, void** work, uint64_t off, uint64_t bytes) {
     const unsigned m = next_pow2(R);
@@ -558,7 +568,10 @@ int fill_dec8(Ff8DecArgs& a, const DeviceTables* t, unsigned K, unsigned R, cons
     a.nunits = uint32_t(bytes / 4);
     bool any_orig = false;
     for (unsigned i = 0; i < K; ++i) any_orig |= orig[i] != nullptr;
-    const bool half = !any_orig && Tn >= 2 && 2 * m == (1u << Tn) && ff8_half_decoder_enabled();
+    const bool two_halves = Tn >= 2 && 2 * m == (1u << Tn);
+    // some originals received: the split decoder (k_ff8_dec_split) when n = 2m
+    if (any_orig) return two_halves && ff8_split_decoder_enabled() ? kDec8Split : kDec8General;
+    const bool half = two_halves && ff8_half_decoder_enabled();
     if (!half) return kDec8General;
     a.fused = t->fused8 + size_t(Tn - 2) * 256 * kTab8Dwords;  // T = Tn - 1, chunk 0
     bool all_rec = K == m && R == m;
@@ -613,7 +626,9 @@ LeopardResult decode_device8(Call& c, uint64_t bytes, uint64_t off, unsigned K, 
     Ff8DecArgs a;
     for (uint64_t pos = 0; pos < bytes; pos += kFf8MaxLaunchBytes) {  // see encode_device
         const int mode = fill_dec8(a, c.t, K, R, orig, rec, work, off + pos, std::min(kFf8MaxLaunchBytes, bytes - pos));
-        HIP_OK(mode != kDec8General ? launch_ff8_decode_half(Tn - 1, a, c.s) : launch_ff8_decode(Tn, a, c.s),
+        HIP_OK(mode == kDec8General ? launch_ff8_decode(Tn, a, c.s)
+               : mode == kDec8Split ? launch_ff8_decode_split(Tn - 1, a, c.s)
+                                    : launch_ff8_decode_half(Tn - 1, a, c.s),
                "decode kernel");
     }
     return Leopard_Success;

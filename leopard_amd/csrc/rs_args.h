@@ -101,7 +101,9 @@ struct Ff8DecArgs {
     __host__ __device__ uint64_t piece(unsigned i) const { return ptr[i]; }
 };
 // GF(2^8) decoder kinds of one argument block (fill_dec8, launch_ff8_decode_batch)
-constexpr int kDec8General = 0, kDec8Half = 1, kDec8HalfDense = 2;
+// (ordered from the least specialised: a batch runs the minimum over its objects;
+// the split decoder also handles the half kinds, with no high-half input)
+constexpr int kDec8General = 0, kDec8Split = 1, kDec8Half = 2, kDec8HalfDense = 3;
 // Forms of the GF(2^8) encoder tile (k_ff8_enc): general (pruned, chunked),
 // dense encode (one chunk, K = R = m), dense inverse (full-loss decode of a
 // K = R = m code, launch_ff8_decode_full).
@@ -117,6 +119,7 @@ struct XorArgs {
 // Launchers (rs_kernels.hip).  Return hipSuccess or the launch error.
 hipError_t launch_decode_hi_half(const DecArgs& a, hipStream_t s);
 hipError_t launch_ff8_decode_half(unsigned Tm, const Ff8DecArgs& a, hipStream_t s);
+hipError_t launch_ff8_decode_split(unsigned Tm, const Ff8DecArgs& a, hipStream_t s);
 hipError_t launch_encode_fused16(unsigned T, const EncArgs& a, hipStream_t s);
 hipError_t launch_encode_lo(const EncArgs& a, hipStream_t s);
 hipError_t launch_encode_hi(const EncArgs& a, hipStream_t s);

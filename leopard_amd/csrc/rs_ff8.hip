@@ -465,6 +465,81 @@ __global__ void __launch_bounds__(threads_for(T, RB), 4) k_ff8_dec_half_batch(co
     ff8_dec_half<T, RB, kDense>(objs[blockIdx.y]);
 }
 
+// Partial loss with n = 2m (K <= m, some originals received).  The received
+// vector splits by linearity into (x, h): x on the low positions (recovery
+// pieces), h on the high ones (surviving originals).  With
+//   F (I + D) I = F_low (swap_top + D_low) I_low      (Tile::derivative_swaptop)
+// and I_low (x, h) = (I_L x, I_H h), the high half -- where every needed output
+// lives -- is
+//   F_H( I_L x  ^  N(I_H h) )
+// with I_L / I_H / F_H the m-point transforms at the skews of the low / high
+// positions and N the m-point neighbour sum of the formal derivative (every
+// tile bit; LeopardFF8.cpp:1890-1899 restricted to one half).  Three m-point
+// transforms on a 2^T tile instead of two n-point ones on a 2^(T+1) tile
+// (k_ff8_dec): every wave busy, a third fewer butterflies.
+template <int T, int RB>
+LDEV void ff8_dec_split(const Ff8DecArgs& a) {
+    if constexpr ((LAMD_ABLATE & 16) != 0) return;
+    using F = FF8;
+    using TL = Tile<F, T, RB, 1>;
+    constexpr unsigned m = 1u << T;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const LdsTab8<256> sk{lds + tile_dwords_for(T, RB)};
+    const LdsTab8<256> ltab{sk.base + LdsTab8<256>::kDwords};  // by log value
+    TabStage8<threads_for(T, RB), 256> sk_stage, log_stage;
+    sk_stage.load(a.sktab);
+    log_stage.load(a.tabs);
+    const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const Cols cl = strip_cols(a.nunits, lane);
+    const PieceSpace low{0, 0, 0}, high{0, 0, m};
+    const Pyr8Live present{a.present}, needed{a.needed};
+    auto lpos = [&](int r) { return TL::piece(0, r, w); };
+    auto hpos = [&](int r) { return m + TL::piece(0, r, w); };
+    typename TL::Reg x, h;
+    {
+        uint64_t pp[TL::NR];
+        fetch_ptrs(pp, a, hpos);
+#pragma unroll
+        for (int r = 0; r < TL::NR; ++r) h[r][0] = present(hpos(r), 0) ? gload(pp[r], cl) : 0u;
+        fetch_ptrs(pp, a, lpos);
+#pragma unroll
+        for (int r = 0; r < TL::NR; ++r) x[r][0] = present(lpos(r), 0) ? gload(pp[r], cl) : 0u;
+    }
+    sk_stage.store(sk);
+    log_stage.store(ltab);
+    __syncthreads();
+    LdsSkew8 win{sk};
+    win.stage(nullptr, -1);  // decoder skew base (LeopardFF8.cpp:1880, 1903)
+    // y = N(I_H(h * exp(el)))
+    scale_batched<TL>(h, ltab, [&](int r) { return el_at(a, hpos(r)); }, [&](int r) { return present(hpos(r), 0); });
+    TL::template ifft<false>(h, w, lane, lds, high, win, present);
+    typename TL::Reg y;
+    TL::zero(y);
+    TL::derivative_add(y, [&](int r, uint32_t* out) { out[0] = h[r][0]; }, w, lane, lds);
+    // x <- I_L(x * exp(el)) ^ y, then F_H
+    scale_batched<TL>(x, ltab, [&](int r) { return el_at(a, lpos(r)); }, [&](int r) { return present(lpos(r), 0); });
+    TL::template ifft<false>(x, w, lane, lds, low, win, present);
+    TL::xor_into(x, y);
+    TL::template fft<false>(x, w, lane, lds, high, win, needed);
+    TL::pin(x);
+    uint64_t pp[TL::NR];
+    fetch_ptrs(pp, a, hpos);
+    auto is_needed = [&](int r) { return needed(hpos(r), 0); };
+    scale_batched<TL>(x, ltab, [&](int r) { return F::kModulus - el_at(a, hpos(r)); }, is_needed);
+    if (!cl.live) return;
+#pragma unroll
+    for (int r = 0; r < TL::NR; ++r)
+        if (is_needed(r)) gstore(pp[r], cl, x[r][0]);
+}
+template <int T, int RB>
+__global__ void __launch_bounds__(threads_for(T, RB), 4) k_ff8_dec_split(Ff8DecArgs a) {
+    ff8_dec_split<T, RB>(a);
+}
+template <int T, int RB>
+__global__ void __launch_bounds__(threads_for(T, RB), 4) k_ff8_dec_split_batch(const Ff8DecArgs* __restrict__ objs) {
+    ff8_dec_split<T, RB>(objs[blockIdx.y]);
+}
+
 // Opting a kernel into > 64 KiB of LDS is a per-function attribute, set once
 // per kernel (Once is a distinct type per kernel instantiation).
 template <class Tag>
@@ -507,6 +582,8 @@ template <int T>
 struct DecBatchTag {};
 template <int T>
 struct DecHalfBatchTag {};
+template <int T>
+struct DecSplitBatchTag {};
 
 template <int T, int RB, bool M, int NA, int G>
 struct EncTag {};
@@ -514,6 +591,8 @@ template <int T, int RB, int NA>
 struct DecTag {};
 template <int T, int RB>
 struct DecHalfTag {};
+template <int T, int RB>
+struct DecSplitTag {};
 
 // Launch shape overrides for experiments (LEO_AMD_FF8_WIDE=1: the wide
 // register forms at every size); read once.
@@ -594,6 +673,12 @@ hipError_t dec_half_T(const Ff8DecArgs& a, hipStream_t s) {
         return launch8<DecHalfTag<T, RB + 16>>(&k_ff8_dec_half<T, RB, true>, threads_for(T, RB), a, lds, s);
     return launch8<DecHalfTag<T, RB>>(&k_ff8_dec_half<T, RB, false>, threads_for(T, RB), a, lds, s);
 }
+template <int T>
+hipError_t dec_split_T(const Ff8DecArgs& a, hipStream_t s) {
+    constexpr int RB = reg_bits8(T);
+    constexpr size_t lds = tile_dwords_for(T, RB) + 2 * LdsTab8<256>::kDwords;
+    return launch8<DecSplitTag<T, RB>>(&k_ff8_dec_split<T, RB>, threads_for(T, RB), a, lds, s);
+}
 
 }  // namespace
 
@@ -650,6 +735,14 @@ hipError_t launch_ff8_decode_half(unsigned Tm, const Ff8DecArgs& a, hipStream_t 
     return e;
 }
 
+hipError_t launch_ff8_decode_split(unsigned Tm, const Ff8DecArgs& a, hipStream_t s) {
+    hipError_t e = hipErrorInvalidValue;
+    static_for<1, 8>([&](auto I) {
+        if (Tm == unsigned(decltype(I)::value)) e = dec_split_T<decltype(I)::value>(a, s);
+    });
+    return e;
+}
+
 hipError_t launch_ff8_encode_batch(unsigned T, const Ff8EncArgs* objs, unsigned count, uint32_t nunits, bool multi,
                                    int form, hipStream_t s) {
     hipError_t e = hipErrorInvalidValue;
@@ -699,7 +792,10 @@ hipError_t launch_ff8_decode_batch(unsigned T, const Ff8DecArgs* objs, unsigned 
             constexpr int TT = decltype(I)::value, RB = batch_bits8(TT);
             constexpr size_t lds = tile_dwords_for(TT, RB) + 2 * LdsTab8<256>::kDwords;
             if (T != unsigned(TT)) return;
-            if (mode == kDec8HalfDense)
+            if (mode == kDec8Split)
+                e = launch8_batch<DecSplitBatchTag<TT>>(&k_ff8_dec_split_batch<TT, RB>, threads_for(TT, RB), objs,
+                                                        count, nunits, lds, s);
+            else if (mode == kDec8HalfDense)
                 e = launch8_batch<DecHalfBatchTag<TT + 16>>(&k_ff8_dec_half_batch<TT, RB, true>, threads_for(TT, RB),
                                                             objs, count, nunits, lds, s);
             else

@@ -98,6 +98,8 @@ DEC_CASES = [  # (K, R, B, originals lost)
     # every original lost with K = R = m: the inverse-transform decoder (launch_ff8_decode_full),
     # single tile (64 KiB-piece form) and the wide form (>= 256 KiB pieces)
     (2, 2, 64, 2), (4, 4, 64 * 3, 4), (16, 16, 64 * 33, 16), (64, 64, 256, 64), (128, 128, 1 << 18, 128),
+    # some originals received with n = 2m: the split decoder (k_ff8_dec_split), K <= m
+    (128, 128, 65536, 16), (60, 40, 64 * 5, 30), (8, 5, 64, 3), (128, 128, 1 << 18, 127), (32, 32, 64, 31),
 ]
 
 
@@ -486,7 +488,8 @@ def _batch_objects(k, r, b, count, seed):
 
 @pytest.mark.parametrize("k,r,b,layout", [(128, 128, 4096, "slab"), (128, 128, 4096, "shuffled"),
                                           (100, 20, 64 * 37, "slab"), (100, 20, 64 * 37, "shuffled"),
-                                          (200, 55, 1024, "slab"), (1000, 200, 256, "slab"), (16, 16, 256, "slab")])
+                                          (200, 55, 1024, "slab"), (1000, 200, 256, "slab"), (16, 16, 256, "slab"),
+                                          (100, 70, 512, "slab")])
 def test_batch_encode_decode_match_oracle(leo, k, r, b, layout):
     """leo_amd_encode_batch / decode_batch (one launch over every object for
     GF(2^8); object by object otherwise) == independent calls == the oracle.

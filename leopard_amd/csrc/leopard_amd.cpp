@@ -134,6 +134,7 @@ struct Workspace {
     // Host-memory pipeline ring: two slots of `slot_bytes` in pinned host memory
     // and in device memory, one stream and two events per slot.
     uint8_t* ring_host = nullptr;
+    uint8_t* ring_host_dev = nullptr;  // device address of ring_host (mapped pinned memory)
     uint8_t* ring_dev = nullptr;
     size_t slot_bytes = 0;
     hipStream_t pipe_stream[2] = {nullptr, nullptr};
@@ -162,12 +163,13 @@ struct Workspace {
             HIP_OK(hipDeviceSynchronize(), "sync before ring growth");
             HIP_OK(hipFree(ring_dev), "free ring");
             HIP_OK(hipHostFree(ring_host), "free pinned ring");
-            ring_dev = ring_host = nullptr;
+            ring_dev = ring_host = ring_host_dev = nullptr;
             slot_bytes = 0;
         }
         const size_t want = (bytes_per_slot + 4095) / 4096 * 4096;
         HIP_OK(hipMalloc(reinterpret_cast<void**>(&ring_dev), 2 * want), "allocate device ring");
         HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&ring_host), 2 * want, hipHostMallocDefault), "pinned ring");
+        HIP_OK(hipHostGetDevicePointer(reinterpret_cast<void**>(&ring_host_dev), ring_host, 0), "map pinned ring");
         slot_bytes = want;
         return Leopard_Success;
     }
@@ -853,12 +855,29 @@ void parallel_copy(const std::vector<CopyJob>& jobs) {
 // [0, nout) of `dout`, row stride `stride`, `len` bytes per row.
 using SliceFn = std::function<LeopardResult(Call&, uint64_t len, uint8_t* din, uint8_t* dout, uint64_t stride)>;
 
+constexpr int kDefaultPipeMode = 0;
+
 // Bytes per ring slot (inputs + outputs of one slice); LEO_AMD_SLOT_MB overrides.
 uint64_t pipe_slot_budget() {
     static const uint64_t v = [] {
         const char* e = std::getenv("LEO_AMD_SLOT_MB");
         const long mb = e ? std::atol(e) : 32;
         return uint64_t(std::max(1L, mb)) << 20;
+    }();
+    return v;
+}
+
+// How a ring slot reaches the kernels (LEO_AMD_PIPE_MODE, read once):
+//   0  SDMA: H2D copy of the inputs, kernels on device memory, D2H copy of the outputs;
+//   1  SDMA H2D of the inputs; the kernels write the outputs straight into the
+//      pinned slot over PCIe (no D2H copy: kernel stores reach ~53 GB/s, the
+//      D2H SDMA engine ~30);
+//   2  the kernels read the inputs from and write the outputs to the pinned slot
+//      over PCIe (no SDMA copies at all).
+int pipe_mode() {
+    static const int v = [] {
+        const char* e = std::getenv("LEO_AMD_PIPE_MODE");
+        return e && e[0] >= '0' && e[0] <= '2' ? e[0] - '0' : kDefaultPipeMode;
     }();
     return v;
 }
@@ -877,6 +896,7 @@ LeopardResult run_host_pipeline(Call& c, uint64_t bytes, const std::vector<const
     if (r != Leopard_Success) return r;
     Workspace& ws = *c.ws;
     const unsigned nslices = unsigned((bytes + slice - 1) / slice);
+    const int mode = pipe_mode();
     auto len_of = [&](unsigned j) { return std::min(slice, bytes - uint64_t(j) * slice); };
     auto scatter = [&](unsigned j) -> LeopardResult {
         const unsigned s = j & 1;
@@ -899,13 +919,20 @@ LeopardResult run_host_pipeline(Call& c, uint64_t bytes, const std::vector<const
         Call cs = c;
         cs.s = ws.pipe_stream[s];
         cs.ws = &workspace(c.dev, cs.s);  // GF(2^16) scratch must not be shared between the two streams
-        HIP_OK(hipMemcpyAsync(dev, pin, in_bytes, hipMemcpyHostToDevice, cs.s), "slice upload");
-        HIP_OK(hipEventRecord(ws.in_done[s], cs.s), "record upload");
-        r = fn(cs, len, dev, dev + in_bytes, slice);
+        uint8_t* mapped = ws.ring_host_dev + s * ws.slot_bytes;  // the pinned slot as the kernels see it
+        if (mode != 2) {
+            HIP_OK(hipMemcpyAsync(dev, pin, in_bytes, hipMemcpyHostToDevice, cs.s), "slice upload");
+            HIP_OK(hipEventRecord(ws.in_done[s], cs.s), "record upload");
+        }
+        r = mode == 0 ? fn(cs, len, dev, dev + in_bytes, slice)
+            : mode == 1 ? fn(cs, len, dev, mapped + in_bytes, slice)
+                        : fn(cs, len, mapped, mapped + in_bytes, slice);
         if (r != Leopard_Success) return r;
         HIP_OK(hipGetLastError(), "kernel launch");
-        HIP_OK(hipMemcpyAsync(pin + in_bytes, dev + in_bytes, nout * slice, hipMemcpyDeviceToHost, cs.s),
-               "slice download");
+        if (mode == 0)
+            HIP_OK(hipMemcpyAsync(pin + in_bytes, dev + in_bytes, nout * slice, hipMemcpyDeviceToHost, cs.s),
+                   "slice download");
+        if (mode == 2) HIP_OK(hipEventRecord(ws.in_done[s], cs.s), "record input use");  // kernels read the slot
         HIP_OK(hipEventRecord(ws.out_done[s], cs.s), "record download");
         if (j >= 1 && (r = scatter(j - 1)) != Leopard_Success) return r;
     }

@@ -501,6 +501,9 @@ LDEV unsigned skew_index(unsigned i, unsigned l) { return ((i >> l) | 1u) << l; 
 // 1/2^S of the tile through an area of 1/2^S the size.  This is what lets two
 // GF(2^16) workgroups of 256 pieces share a CU's 160 KiB of LDS, so that one
 // workgroup's loads and stores overlap the other's butterflies.
+#ifndef LAMD_FF8_KB
+#define LAMD_FF8_KB 4  // FF8 butterfly tables read (and live) together per layer batch
+#endif
 template <class F, int T, int R, int C, int LW = 64, int S = 0>
 struct Tile {
     static_assert(R >= 1 && R <= T, "register bits");
@@ -627,7 +630,7 @@ struct Tile {
             // FF8 (5-dword tables): read every table of the layer, then let the
             // scheduler interleave the layer's independent butterflies (ILP).
             // At most 4 tables (20 VGPRs) live at a time.
-            constexpr int KB = NG < 4 ? NG : 4;
+            constexpr int KB = NG < LAMD_FF8_KB ? NG : LAMD_FF8_KB;
             static_for<0, NG / KB>([&](auto BI) {
                 constexpr int g0 = decltype(BI)::value * KB;
                 typename F::Tab tabs[KB];

@@ -294,8 +294,11 @@ __global__ void __launch_bounds__(threads_for(T, RB), 4) k_ff8_enc_batch(const F
 
 // Slab batch (leo_amd_encode_batch / decode_batch on slab-laid objects): the
 // argument block of every object is in the kernel arguments, object blockIdx.y.
+#ifndef LAMD_SLAB_WAVES
+#define LAMD_SLAB_WAVES 4
+#endif
 template <int T, int RB, bool kMulti, int kForm = kFormGeneral>
-__global__ void __launch_bounds__(threads_for(T, RB), 4) k_ff8_enc_slab(Ff8SlabBatch b) {
+__global__ void __launch_bounds__(threads_for(T, RB), LAMD_SLAB_WAVES) k_ff8_enc_slab(Ff8SlabBatch b) {
     ff8_enc<T, RB, kMulti, 1, 0, kForm>(Ff8SlabView(b, blockIdx.y));
 }
 

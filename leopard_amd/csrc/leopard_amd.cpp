@@ -653,8 +653,6 @@ LeopardResult decode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
     for (unsigned i = 0; i < K; ++i)
         if (!orig[i]) set(m + i);
 
-
-
     DecArgs a;
     std::memset(&a, 0, sizeof(a));
     MapBuilder mb;

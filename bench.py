@@ -80,6 +80,8 @@ def parse():
     ap.add_argument("--mode", choices=("batch", "calls"), default="batch",
                     help="batch: a step is one leo_amd_encode_batch + one leo_amd_decode_batch over its objects "
                          "(one launch each); calls: one leo_encode + leo_decode per object, S streams in flight")
+    ap.add_argument("--batch-streams", type=int, default=2,
+                    help="batch mode: consecutive steps alternate over this many streams")
     ap.add_argument("--sharded-steps", type=int, default=0, help="steps of the configs[4] object (0 = min(steps, 10))")
     ap.add_argument("--no-sharded", action="store_true", help="skip the configs[4] sharded object")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -206,7 +208,8 @@ def main():
             "data": "synthetic (counter-hash bytes on device)",
             "config": {"workload": f"configs[1]: {k}+{r} x {nbytes} B pieces, GF(2^8); step = {args.objects} objects "
                                    f"per rank, each encoded then decoded with all {k} originals lost, "
-                                   + ("one batched encode + decode launch per step"
+                                   + (f"one batched encode + decode launch per step, consecutive steps on "
+                                      f"{args.batch_streams} streams"
                                       if args.mode == "batch" else f"{head['streams']} objects in flight")
                                    + f"; {head['sets']} rotating buffer sets"
                                    + (f"; plus configs[4] (sharded_object): one 32768+32768 x 65536 B object "
@@ -241,7 +244,7 @@ def headline(args, leo, torch, device, barrier, world, max_over_ranks):
     stream = torch.cuda.current_stream(device)
     k, r, nbytes = args.K, args.R, args.bytes
     per_set = (k + leo.leo_encode_work_count(k, r) + leo.leo_decode_work_count(k, r)) * nbytes
-    nsets = args.sets or max(16, args.objects, -(-(512 << 20) // per_set))
+    nsets = args.sets or max(16, args.objects * max(1, args.batch_streams), -(-(512 << 20) // per_set))
     sets = Sets(leo, torch, k, r, nbytes, nsets, device)
     torch.cuda.synchronize()
 
@@ -286,9 +289,13 @@ def headline(args, leo, torch, device, barrier, world, max_over_ranks):
                         mk([sets.p_null[i] for i in ids]), mk([sets.p_rec[i] for i in ids]),
                         mk([sets.p_decw[i] for i in ids])))
 
+    # Consecutive steps alternate over --batch-streams streams (their buffer
+    # sets differ), so one step's encode overlaps the previous step's decode tail.
+    bstreams = [stream] + [torch.cuda.Stream(device) for _ in range(max(1, args.batch_streams) - 1)]
+
     def run_batches(nsteps, _ns):
-        leo.set_stream(stream.cuda_stream)
         for s in range(nsteps):
+            leo.set_stream(bstreams[s % len(bstreams)].cuda_stream)
             bo, bw, bn, br, bd = batches[s % nbatches]
             if (lib.leo_amd_encode_batch(args.objects, nbytes, k, r, sets.enc_wc, bo, bw) != 0 or
                     lib.leo_amd_decode_batch(args.objects, nbytes, k, r, sets.dec_wc, bn, br, bd) != 0):
@@ -353,7 +360,7 @@ def headline(args, leo, torch, device, barrier, world, max_over_ranks):
            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
            "modes": {
                "batch": rate(elapsed_batch, "leo_amd_encode_batch + leo_amd_decode_batch over the step's objects, "
-                                            "one launch each, one stream"),
+                                            f"one launch each; consecutive steps on {len(bstreams)} stream(s)"),
                "calls_in_flight": rate(elapsed_calls, f"one leo_encode + leo_decode per object, {nstreams} objects "
                                                       f"in flight on {nstreams} streams"),
                "serial": rate(elapsed_serial, "one leo_encode + leo_decode per object on one stream: each call "

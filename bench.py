@@ -23,12 +23,15 @@ leo_amd_encode_slice / leo_amd_decode_slice on its B/N columns of every piece
 fixed as N grows).  With N > 1, rank 0 also times the whole object alone on
 its GPU in the same run, so the line carries the 1-GPU time of that object.
 
-Roofline: the dominant kernel of the headline is timed alone with HIP events
-on the stream it runs on (back-to-back calls queued behind a spin kernel);
-achieved = algorithmic bytes per launch ((K + R) * B encode, (K_surv + lost) *
-B decode) / mean launch duration, against the 8 TB/s HBM3E
-peak.  traffic = HBM bytes per launch from the committed rocprofv3 PMC pass
-(tools/pmc_traffic.py), when present for this workload.
+Roofline: the dominant kernel of the headline's timed region (batch mode: the
+encode-batch or decode-batch launch, k_ff8_enc_slab, whichever is longer) is
+timed alone with HIP events on the stream it runs on (back-to-back launches
+queued behind a spin kernel); achieved = algorithmic bytes per launch (objects
+x ((K + R) * B encode, (K_surv + lost) * B decode)) / mean
+launch duration, against the 8 TB/s HBM3E peak.  traffic = HBM bytes per
+launch from the committed rocprofv3 PMC pass (tools/pmc_traffic.py), when
+present for this workload.  roofline.single_call carries the same figures for
+one leo_encode / leo_decode call (the plain drop-in caller's kernel).
 
 cpu_baseline: the reference library compiled from its sources
 (oracle/_ref/libleopard_ref.so, AVX2 + OpenMP) on this host: the headline
@@ -190,9 +193,15 @@ def main():
 
     if rank == 0:
         k, r, nbytes = args.K, args.R, args.bytes
-        traffic = pmc_traffic(head["dominant"][0], k, r, nbytes)
+        batch = args.mode == "batch"
+        traffic = pmc_traffic(head["dominant"][0], k, r, nbytes, args.objects if batch else 1)
         kind, algo, t_kernel = head["dominant"]
         achieved = algo / t_kernel / 1e9
+        s_kind, s_algo, s_t = head["single_dominant"]
+        s_traffic = pmc_traffic(s_kind, k, r, nbytes, 1)
+        kname = ("k_ff8_enc_slab<7,4,false,%d>: one %d-object batch launch (%s)"
+                 % (2 if kind == "decode" else 1, args.objects, "full-loss decode form" if kind == "decode"
+                    else "dense encode form")) if batch else kind
         out = {
             "metric": "device-resident encode+decode GB/s (input bytes/s) at 128+128 and 32768+32768 pieces",
             "value": head["value"],
@@ -224,10 +233,17 @@ def main():
             "decode_GBps": round(k * nbytes / head["t_dec"] / 1e9, 3),
             "encode_us": round(head["t_enc"] * 1e6, 3),
             "decode_us": round(head["t_dec"] * 1e6, 3),
-            "roofline": {"bound": "hbm", "kernel": kind, "achieved": round(achieved, 2),
+            "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "traffic": traffic.get("bytes"), "traffic_source": traffic.get("source"),
-                         "algorithmic_bytes_per_launch": algo},
+                         "algorithmic_bytes_per_launch": algo, "launch_us": round(t_kernel * 1e6, 3),
+                         "batch_encode_us": round(head["tb_enc"] * 1e6, 3),
+                         "batch_decode_us": round(head["tb_dec"] * 1e6, 3),
+                         "single_call": {"kernel": s_kind, "launch_us": round(s_t * 1e6, 3),
+                                         "achieved": round(s_algo / s_t / 1e9, 2),
+                                         "frac": round(s_algo / s_t / 1e9 / HBM_PEAK_GBPS, 4),
+                                         "traffic": s_traffic.get("bytes"), "traffic_source": s_traffic.get("source"),
+                                         "algorithmic_bytes_per_launch": s_algo}},
             "cpu_baseline": cpu,
             "sharded_object": sharded,
             "host_e2e": host,
@@ -350,6 +366,38 @@ def headline(args, leo, torch, device, barrier, world, max_over_ranks):
     algo_enc = (k + r) * nbytes
     algo_dec = (r + k) * nbytes  # R surviving pieces read + K lost originals written (full loss)
     dominant = ("decode", algo_dec, t_dec) if t_dec >= t_enc else ("encode", algo_enc, t_enc)
+
+    # The batch mode's kernels (the headline's timed region: one encode-batch and
+    # one decode-batch launch per step), timed the same way: back-to-back launches
+    # behind a spin kernel on the launch stream, time / n = mean launch duration.
+    def time_batch(decode, n=20):
+        leo.set_stream(stream.cuda_stream)
+
+        def launch(j):
+            bo, bw, bn, br, bd = batches[j % nbatches]
+            rc = (lib.leo_amd_decode_batch(args.objects, nbytes, k, r, sets.dec_wc, bn, br, bd) if decode
+                  else lib.leo_amd_encode_batch(args.objects, nbytes, k, r, sets.enc_wc, bo, bw))
+            if rc != 0:
+                raise RuntimeError(leo.last_error())
+        for j in range(3):
+            launch(j)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda._sleep(50_000_000)
+        e0.record(stream)
+        for j in range(n):
+            launch(j)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / 1e3 / n
+
+    tb_enc, tb_dec = time_batch(False), time_batch(True)
+    algo_batch = args.objects * (k + r) * nbytes
+    batch_dominant = (("decode", algo_batch, tb_dec) if tb_dec >= tb_enc else ("encode", algo_batch, tb_enc))
+    if args.mode == "batch":
+        dominant, single_dominant = batch_dominant, dominant
+    else:
+        single_dominant = dominant
     in_step = k * nbytes * args.objects
 
     def rate(el, note):
@@ -365,7 +413,8 @@ def headline(args, leo, torch, device, barrier, world, max_over_ranks):
                                                       f"in flight on {nstreams} streams"),
                "serial": rate(elapsed_serial, "one leo_encode + leo_decode per object on one stream: each call "
                                               "waits for the previous (a plain drop-in caller)")},
-           "t_enc": t_enc, "t_dec": t_dec, "dominant": dominant, "sets": sets.n, "streams": nstreams}
+           "t_enc": t_enc, "t_dec": t_dec, "tb_enc": tb_enc, "tb_dec": tb_dec, "dominant": dominant,
+           "single_dominant": single_dominant, "sets": sets.n, "streams": nstreams}
     del sets
     torch.cuda.empty_cache()
     return res
@@ -544,18 +593,19 @@ def host_e2e_run(leo, k, r, nbytes, steps, register):
             "sample": f"{steps} steps of {k}+{r} x {nbytes} B encode + full-loss decode, {how}"}
 
 
-def pmc_traffic(kernel, k, r, nbytes):
+def pmc_traffic(kernel, k, r, nbytes, objects=1):
     """HBM bytes per launch of the dominant kernel from the committed PMC pass
     (tools/pmc_traffic.py: FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md HBM
     section), when one exists for this workload; else None."""
     import glob
-    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*", "pmc_traffic.json")), reverse=True):
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*", "pmc_traffic*.json")), reverse=True):
         try:
             with open(path) as f:
                 d = json.load(f)
         except (OSError, ValueError):
             continue
-        e = d.get("workloads", {}).get(f"{k}+{r}x{nbytes}", {}).get(kernel)
+        key = f"{k}+{r}x{nbytes}" + (f"/batch{objects}" if objects > 1 else "")
+        e = d.get("workloads", {}).get(key, {}).get(kernel)
         if e:
             return {"bytes": e["hbm_bytes_per_launch"], "source": os.path.relpath(path, REPO)}
     return {}

@@ -3,6 +3,8 @@
 
 GPU box:  KB_ARGS="128 128 65536" bash tools/pmc.sh FETCH_SIZE WRITE_SIZE
           python3 tools/pmc_traffic.py 128 128 65536 gpurun_out/pmc1 gpurun_out/pmc2 > profiles/<round>/pmc_traffic.json
+Batched launches:  PMC_TOOL=bbench KB_ARGS="128 128 65536 16" bash tools/pmc.sh FETCH_SIZE WRITE_SIZE
+          python3 tools/pmc_traffic.py --objects 16 128 128 65536 gpurun_out/pmc1 gpurun_out/pmc2
 
 FETCH_SIZE and WRITE_SIZE are KiB per dispatch.  On gfx950 FETCH_SIZE counts
 half the bytes of coalesced streaming reads (MI355X_MICROARCH.md, HBM section),
@@ -18,7 +20,12 @@ from collections import defaultdict
 
 
 def kernel_kind(name):
-    if "k_ff8_enc" in name or "k_enc" in name:
+    # the GF(2^8) encoder tile also runs full-loss decodes of K = R = m codes:
+    # its last template argument is the form (rs_args.h: 1 dense encode, 2 dense decode)
+    m = re.search(r"k_ff8_enc(?:_slab|_batch)?<([^>]*)>", name)
+    if m:
+        return "decode" if m.group(1).split(",")[-1].strip() == "2" else "encode"
+    if "k_enc" in name:
         return "encode"
     if "k_ff8_dec" in name or "k_dec" in name:
         return "decode"
@@ -26,8 +33,13 @@ def kernel_kind(name):
 
 
 def main():
-    k, r, b = (int(x) for x in sys.argv[1:4])
-    dirs = sys.argv[4:]
+    args = sys.argv[1:]
+    objects = 1
+    if args[0] == "--objects":  # batched launches (tools/bbench.py): bytes of every object of a launch
+        objects = int(args[1])
+        args = args[2:]
+    k, r, b = (int(x) for x in args[:3])
+    dirs = args[3:]
     vals = defaultdict(lambda: defaultdict(list))
     names = {}
     for d in dirs:
@@ -45,8 +57,9 @@ def main():
         out[kind] = {"kernel": names[kind], "FETCH_SIZE_KiB": round(fetch, 1), "WRITE_SIZE_KiB": round(write, 1),
                      "dispatches": len(cs["FETCH_SIZE"]),
                      "hbm_bytes_per_launch": int((2 * fetch + write) * 1024),
-                     "algorithmic_bytes_per_launch": (k + r) * b}
-    print(json.dumps({"workloads": {f"{k}+{r}x{b}": out},
+                     "algorithmic_bytes_per_launch": objects * (k + r) * b}
+    key = f"{k}+{r}x{b}" + (f"/batch{objects}" if objects > 1 else "")
+    print(json.dumps({"workloads": {key: out},
                       "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes; (2*FETCH+WRITE) KiB"},
                      indent=1))
 

@@ -177,6 +177,12 @@ constexpr unsigned threads16(int T, int R) { return 64u << (T - R); }
 template <int T, int R, int S>
 using Tile16 = Tile<FF16, T, R, C, 64, S>;
 
+// Waves per SIMD the high passes are compiled for (4: <= 128 VGPRs; 3 gives
+// the 32-piece tiles room without spills at one workgroup fewer per CU).
+#ifndef LAMD_HI_WAVES
+#define LAMD_HI_WAVES 4
+#endif
+
 // Pruning inside a multi-pass tile: off by default.  A per-group branch around
 // updates of a 64-VGPR tile makes the register allocator copy and spill at
 // every merge; every butterfly runs instead (a dead IFFT block is all zero and
@@ -256,7 +262,7 @@ __global__ void __launch_bounds__(threads16(kLoBits, R), 4) k_enc_lo(EncArgs a) 
 // tables of chunk c (skew base m-1 + c*m) and the FFT tables (base -1) are two
 // LDS sets.  kMulti: several chunks (T <= 6 then), accumulated in a second tile.
 template <int T, int R, int S, bool kMulti>
-__global__ void __launch_bounds__(threads16(T, R), 4) k_enc_hi(EncArgs a) {
+__global__ void __launch_bounds__(threads16(T, R), LAMD_HI_WAVES) k_enc_hi(EncArgs a) {
     constexpr int NT = threads16(T, R);
     using TL = Tile16<T, R, S>;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -423,7 +429,7 @@ __global__ void __launch_bounds__(threads16(kLoBits, R), 4) k_dec_lo(DecArgs a) 
 // The other term of the split derivative needs F_hi(I_hi U) = U, which pass 3
 // reads straight from pass 1's slab.  Tables: skew base -1, positions j << 8.
 template <int T, int R, int S>
-__global__ void __launch_bounds__(threads16(T, R), 4) k_dec_hi(DecArgs a) {
+__global__ void __launch_bounds__(threads16(T, R), LAMD_HI_WAVES) k_dec_hi(DecArgs a) {
     constexpr int NT = threads16(T, R);
     using TL = Tile16<T, R, S>;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -463,7 +469,7 @@ __global__ void __launch_bounds__(threads16(T, R), 4) k_dec_hi(DecArgs a) {
 // positions only and pass 3 adds D_lo(U) = 0 there (U has no high tiles).
 // Tables: skew base -1, positions j << 8 (low half) and m + (j << 8) (high half).
 template <int T, int R, int S>
-__global__ void __launch_bounds__(threads16(T, R), 4) k_dec_hi_half(DecArgs a) {
+__global__ void __launch_bounds__(threads16(T, R), LAMD_HI_WAVES) k_dec_hi_half(DecArgs a) {
     constexpr int NT = threads16(T, R);
     using TL = Tile16<T, R, S>;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];

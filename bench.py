@@ -76,7 +76,9 @@ def parse():
     ap.add_argument("--K", type=int, default=128)
     ap.add_argument("--R", type=int, default=128)
     ap.add_argument("--bytes", type=int, default=65536)
-    ap.add_argument("--objects", type=int, default=16, help="independent objects per step")
+    ap.add_argument("--objects", type=int, default=64, help="independent objects per step")
+    ap.add_argument("--launch-objects", type=int, default=16,
+                    help="batch mode: objects per leo_amd_*_batch launch (a step is objects / launch-objects launches)")
     ap.add_argument("--sets", type=int, default=0, help="buffer sets rotated (0 = enough for >512 MiB)")
     ap.add_argument("--streams", type=int, default=3,
                     help="per-call mode: object o of a step runs on HIP stream o %% S")
@@ -194,13 +196,13 @@ def main():
     if rank == 0:
         k, r, nbytes = args.K, args.R, args.bytes
         batch = args.mode == "batch"
-        traffic = pmc_traffic(head["dominant"][0], k, r, nbytes, args.objects if batch else 1)
+        traffic = pmc_traffic(head["dominant"][0], k, r, nbytes, head["launch_objects"] if batch else 1)
         kind, algo, t_kernel = head["dominant"]
         achieved = algo / t_kernel / 1e9
         s_kind, s_algo, s_t = head["single_dominant"]
         s_traffic = pmc_traffic(s_kind, k, r, nbytes, 1)
         kname = ("k_ff8_enc_slab<7,4,false,%d>: one %d-object batch launch (%s)"
-                 % (2 if kind == "decode" else 1, args.objects, "full-loss decode form" if kind == "decode"
+                 % (2 if kind == "decode" else 1, head["launch_objects"], "full-loss decode form" if kind == "decode"
                     else "dense encode form")) if batch else kind
         out = {
             "metric": "device-resident encode+decode GB/s (input bytes/s) at 128+128 and 32768+32768 pieces",
@@ -217,14 +219,14 @@ def main():
             "data": "synthetic (counter-hash bytes on device)",
             "config": {"workload": f"configs[1]: {k}+{r} x {nbytes} B pieces, GF(2^8); step = {args.objects} objects "
                                    f"per rank, each encoded then decoded with all {k} originals lost, "
-                                   + (f"one batched encode + decode launch per step, consecutive steps on "
-                                      f"{args.batch_streams} streams"
+                                   + (f"batched encode + decode launches of {head['launch_objects']} objects, "
+                                      f"consecutive launch pairs on {args.batch_streams} streams"
                                       if args.mode == "batch" else f"{head['streams']} objects in flight")
                                    + f"; {head['sets']} rotating buffer sets"
                                    + (f"; plus configs[4] (sharded_object): one 32768+32768 x 65536 B object "
                                       f"column-sharded over {world} GPUs" if sharded else ""),
                        "original_count": k, "recovery_count": r, "buffer_bytes": nbytes, "losses": k,
-                       "objects_per_step": args.objects, "mode": args.mode,
+                       "objects_per_step": args.objects, "objects_per_launch": head["launch_objects"], "mode": args.mode,
                        "field": "FF8" if leo.leo_decode_work_count(k, r) <= 256 else "FF16",
                        "sharding": "objects per rank (headline); 64-byte column blocks per rank (sharded_object); "
                                    "no collective"},
@@ -260,7 +262,8 @@ def headline(args, leo, torch, device, barrier, world, max_over_ranks):
     stream = torch.cuda.current_stream(device)
     k, r, nbytes = args.K, args.R, args.bytes
     per_set = (k + leo.leo_encode_work_count(k, r) + leo.leo_decode_work_count(k, r)) * nbytes
-    nsets = args.sets or max(16, args.objects * max(1, args.batch_streams), -(-(512 << 20) // per_set))
+    lobj = max(1, min(args.launch_objects, args.objects))
+    nsets = args.sets or max(16, args.objects, lobj * max(1, args.batch_streams), -(-(512 << 20) // per_set))
     sets = Sets(leo, torch, k, r, nbytes, nsets, device)
     torch.cuda.synchronize()
 
@@ -292,30 +295,34 @@ def headline(args, leo, torch, device, barrier, world, max_over_ranks):
                 if enc(i) != 0 or dec(i) != 0:
                     raise RuntimeError(leo.last_error())
 
-    # Batch mode: step s covers buffer sets (s * objects + o) % n, o < objects:
-    # one leo_amd_encode_batch and one leo_amd_decode_batch (one kernel launch
-    # each) on one stream; the pointer arrays are built once per distinct batch.
+    # Batch mode: step s covers buffer sets (s * objects + o) % n, o < objects,
+    # in launches of lobj objects: one leo_amd_encode_batch and one
+    # leo_amd_decode_batch (one kernel launch each) per group, consecutive groups
+    # alternating over --batch-streams streams (their buffer sets differ, so one
+    # group's encode overlaps the previous group's decode tail); the pointer
+    # arrays are built once per distinct group.
     PP = ctypes.POINTER(VP)
-    nbatches = sets.n // max(1, args.objects) if sets.n % max(1, args.objects) == 0 else sets.n
+    nbatches = sets.n // lobj if sets.n % lobj == 0 else sets.n
     batches = []
     for bi in range(nbatches):
-        ids = [(bi * args.objects + o) % sets.n for o in range(args.objects)]
+        ids = [(bi * lobj + o) % sets.n for o in range(lobj)]
         mk = lambda arrs: (PP * len(arrs))(*[ctypes.cast(a, PP) for a in arrs])  # noqa: E731
         batches.append((mk([sets.p_orig[i] for i in ids]), mk([sets.p_encw[i] for i in ids]),
                         mk([sets.p_null[i] for i in ids]), mk([sets.p_rec[i] for i in ids]),
                         mk([sets.p_decw[i] for i in ids])))
-
-    # Consecutive steps alternate over --batch-streams streams (their buffer
-    # sets differ), so one step's encode overlaps the previous step's decode tail.
     bstreams = [stream] + [torch.cuda.Stream(device) for _ in range(max(1, args.batch_streams) - 1)]
+    groups = -(-args.objects // lobj)
 
     def run_batches(nsteps, _ns):
         for s in range(nsteps):
-            leo.set_stream(bstreams[s % len(bstreams)].cuda_stream)
-            bo, bw, bn, br, bd = batches[s % nbatches]
-            if (lib.leo_amd_encode_batch(args.objects, nbytes, k, r, sets.enc_wc, bo, bw) != 0 or
-                    lib.leo_amd_decode_batch(args.objects, nbytes, k, r, sets.dec_wc, bn, br, bd) != 0):
-                raise RuntimeError(leo.last_error())
+            for g in range(groups):
+                j = s * groups + g
+                cnt = min(lobj, args.objects - g * lobj)
+                leo.set_stream(bstreams[j % len(bstreams)].cuda_stream)
+                bo, bw, bn, br, bd = batches[(s * args.objects // lobj + g) % nbatches]
+                if (lib.leo_amd_encode_batch(cnt, nbytes, k, r, sets.enc_wc, bo, bw) != 0 or
+                        lib.leo_amd_decode_batch(cnt, nbytes, k, r, sets.dec_wc, bn, br, bd) != 0):
+                    raise RuntimeError(leo.last_error())
 
     def timed(run, ns):
         run(args.warmup, ns)
@@ -375,8 +382,8 @@ def headline(args, leo, torch, device, barrier, world, max_over_ranks):
 
         def launch(j):
             bo, bw, bn, br, bd = batches[j % nbatches]
-            rc = (lib.leo_amd_decode_batch(args.objects, nbytes, k, r, sets.dec_wc, bn, br, bd) if decode
-                  else lib.leo_amd_encode_batch(args.objects, nbytes, k, r, sets.enc_wc, bo, bw))
+            rc = (lib.leo_amd_decode_batch(lobj, nbytes, k, r, sets.dec_wc, bn, br, bd) if decode
+                  else lib.leo_amd_encode_batch(lobj, nbytes, k, r, sets.enc_wc, bo, bw))
             if rc != 0:
                 raise RuntimeError(leo.last_error())
         for j in range(3):
@@ -392,7 +399,7 @@ def headline(args, leo, torch, device, barrier, world, max_over_ranks):
         return e0.elapsed_time(e1) / 1e3 / n
 
     tb_enc, tb_dec = time_batch(False), time_batch(True)
-    algo_batch = args.objects * (k + r) * nbytes
+    algo_batch = lobj * (k + r) * nbytes
     batch_dominant = (("decode", algo_batch, tb_dec) if tb_dec >= tb_enc else ("encode", algo_batch, tb_enc))
     if args.mode == "batch":
         dominant, single_dominant = batch_dominant, dominant
@@ -407,14 +414,15 @@ def headline(args, leo, torch, device, barrier, world, max_over_ranks):
     res = {"value": round(world * in_step * args.steps / elapsed / 1e9, 3),
            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
            "modes": {
-               "batch": rate(elapsed_batch, "leo_amd_encode_batch + leo_amd_decode_batch over the step's objects, "
-                                            f"one launch each; consecutive steps on {len(bstreams)} stream(s)"),
+               "batch": rate(elapsed_batch, f"leo_amd_encode_batch + leo_amd_decode_batch per {lobj} objects "
+                                            f"(one launch each), {groups} launch pairs per step, consecutive pairs "
+                                            f"on {len(bstreams)} stream(s)"),
                "calls_in_flight": rate(elapsed_calls, f"one leo_encode + leo_decode per object, {nstreams} objects "
                                                       f"in flight on {nstreams} streams"),
                "serial": rate(elapsed_serial, "one leo_encode + leo_decode per object on one stream: each call "
                                               "waits for the previous (a plain drop-in caller)")},
            "t_enc": t_enc, "t_dec": t_dec, "tb_enc": tb_enc, "tb_dec": tb_dec, "dominant": dominant,
-           "single_dominant": single_dominant, "sets": sets.n, "streams": nstreams}
+           "single_dominant": single_dominant, "sets": sets.n, "streams": nstreams, "launch_objects": lobj}
     del sets
     torch.cuda.empty_cache()
     return res

@@ -603,3 +603,65 @@ def test_registered_host_memory_in_place(leo, k, r, b, loss):
         for arr in (data, work, dwork):
             assert leo.unregister_host(arr.ctypes.data) == leo.LeopardResult.Success
     assert leo.unregister_host(data.ctypes.data) == leo.LeopardResult.InvalidInput
+
+
+# ------------------------------------------------------------ reentrancy --
+
+def test_concurrent_host_threads_are_reentrant(leo):
+    """The reference's encode/decode are reentrant (tables read-only after
+    init, state on the stack: SURVEY.md 8(b), leopard.cpp:123-344).  Here each
+    host thread has its own stream and scratch: 4 threads call leo_encode /
+    leo_decode at once (ctypes drops the GIL) on host buffers and device
+    buffers, GF(2^8) and GF(2^16) shapes, and every result must equal the
+    oracle's."""
+    import threading
+
+    shapes = [(128, 128, 4096), (1000, 200, 256), (100, 20, 640), (300, 300, 128)]
+    jobs = []
+    for t, (k, r, b) in enumerate(shapes):
+        rng = np.random.default_rng(100 + t)
+        data = rng.integers(0, 256, (k, b), dtype=np.uint8)
+        loss = min(k, r) // 2 + 1
+        lo = sorted(rng.choice(k, loss, replace=False).tolist())
+        lr = sorted(rng.choice(r, r - loss, replace=False).tolist())
+        jobs.append(dict(k=k, r=r, b=b, data=data, rec=ol.oracle().encode(data, r), lo=lo, lr=lr))
+    errors = []
+
+    def worker(job, device):
+        try:
+            k, r, b = job["k"], job["r"], job["b"]
+            wc, dwc = leo.leo_encode_work_count(k, r), leo.leo_decode_work_count(k, r)
+            for it in range(6):
+                if device:
+                    data = torch.from_numpy(job["data"]).cuda()
+                    work = torch.zeros((wc, b), dtype=torch.uint8, device="cuda")
+                    dwork = torch.zeros((dwc, b), dtype=torch.uint8, device="cuda")
+                    ptr = lambda t, i: t[i].data_ptr()  # noqa: E731
+                else:
+                    data = job["data"]
+                    work = np.zeros((wc, b), dtype=np.uint8)
+                    dwork = np.zeros((dwc, b), dtype=np.uint8)
+                    ptr = lambda t, i: t[i].ctypes.data  # noqa: E731
+                torch.cuda.synchronize()
+                res = leo.leo_encode(b, k, r, wc, [ptr(data, i) for i in range(k)], [ptr(work, i) for i in range(wc)])
+                assert res == leo.LeopardResult.Success, leo.last_error()
+                rec = work[:r].cpu().numpy() if device else work[:r]
+                assert np.array_equal(rec, job["rec"]), ("encode", k, r, it, device)
+                res = leo.leo_decode(b, k, r, dwc, [None if i in job["lo"] else ptr(data, i) for i in range(k)],
+                                     [None if i in job["lr"] else ptr(work, i) for i in range(r)],
+                                     [ptr(dwork, i) for i in range(dwc)])
+                assert res == leo.LeopardResult.Success, leo.last_error()
+                got = dwork.cpu().numpy() if device else dwork
+                for i in job["lo"]:
+                    assert np.array_equal(got[i], job["data"][i]), ("decode", k, r, it, device, i)
+        except BaseException as e:  # noqa: BLE001 -- reported by the main thread
+            errors.append(repr(e))
+
+    for device in (False, True):
+        threads = [threading.Thread(target=worker, args=(job, device)) for job in jobs]
+        for th in threads:
+            th.start()
+        for th in threads:
+            th.join(timeout=90)
+        assert not any(th.is_alive() for th in threads), "a worker thread hung"
+    assert not errors, errors

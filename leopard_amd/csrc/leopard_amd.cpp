@@ -1341,12 +1341,15 @@ bool batch_on_device(unsigned count, const void* const* firsts, int* dev) {
     return true;
 }
 
-// Pieces p[0, n) equally spaced (a slab): base and stride (two's complement).
-bool slab_of(const void* const* p, unsigned n, uint64_t& base, uint64_t& stride) {
+// Pieces p[0, n) equally spaced (a slab) with a stride that fits a signed
+// 32-bit integer (Ff8SlabBatch): base and stride (two's complement).
+bool slab_of(const void* const* p, unsigned n, uint64_t& base, int32_t& stride) {
     base = uint64_t(reinterpret_cast<uintptr_t>(p[0]));
-    stride = n > 1 ? uint64_t(reinterpret_cast<uintptr_t>(p[1])) - base : 0;
+    const int64_t s = n > 1 ? int64_t(uint64_t(reinterpret_cast<uintptr_t>(p[1])) - base) : 0;
+    if (s < INT32_MIN || s > INT32_MAX) return false;
+    stride = int32_t(s);
     for (unsigned i = 0; i < n; ++i)
-        if (!p[i] || uint64_t(reinterpret_cast<uintptr_t>(p[i])) != base + uint64_t(i) * stride) return false;
+        if (!p[i] || uint64_t(reinterpret_cast<uintptr_t>(p[i])) != base + uint64_t(int64_t(i) * s)) return false;
     return true;
 }
 
@@ -1357,7 +1360,8 @@ bool slab_of(const void* const* p, unsigned n, uint64_t& base, uint64_t& stride)
 bool run_slab_batch8(int dev, unsigned count, uint64_t bytes, unsigned T, unsigned K, unsigned R, unsigned nin,
                      unsigned nout, const void* const* const* ins, void* const* const* outs, bool multi, int form,
                      LeopardResult* res) {
-    std::vector<uint64_t> ib(count), is(count), ob(count), os(count);
+    std::vector<uint64_t> ib(count), ob(count);
+    std::vector<int32_t> is(count), os(count);
     for (unsigned o = 0; o < count; ++o)
         if (!slab_of(ins[o], nin, ib[o], is[o]) ||
             !slab_of(const_cast<const void* const*>(outs[o]), nout, ob[o], os[o]))

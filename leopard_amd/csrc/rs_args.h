@@ -59,15 +59,20 @@ struct Ff8EncArgs {
     unsigned K, R, nchunks;
     uint32_t nunits;         // dword columns per piece in this launch
     __host__ __device__ uint64_t piece(unsigned i) const { return ptr[i]; }
+    static constexpr bool kSlab = false;
+    __host__ __device__ uint64_t in_piece(unsigned i) const { return ptr[i]; }       // i < K
+    __host__ __device__ uint64_t out_piece(unsigned j) const { return ptr[K + j]; }  // j < R
 };
 // Batches whose objects keep their pieces in slabs (piece i at base + i *
 // stride, the usual layout of a caller's buffer): the whole batch travels by
 // value in the kernel arguments -- no argument upload in front of the launch.
 // Encoder tile view (Ff8SlabView): pieces [0, K) = in slab, [K, K + R) = out slab.
+// Strides are signed 32-bit (the host falls back to pointer tables otherwise):
+// a piece address is one 32 x 32 -> 64-bit scalar multiply and a 64-bit add.
 constexpr unsigned kSlabObjs = 64;
 struct Ff8SlabBatch {
-    uint64_t in_base[kSlabObjs], in_stride[kSlabObjs];    // column base of the launch applied
-    uint64_t out_base[kSlabObjs], out_stride[kSlabObjs];
+    uint64_t in_base[kSlabObjs], out_base[kSlabObjs];  // column base of the launch applied
+    int32_t in_stride[kSlabObjs], out_stride[kSlabObjs];
     const uint32_t* sktab;
     const uint32_t* fused;
     unsigned K, R, nchunks;
@@ -75,17 +80,19 @@ struct Ff8SlabBatch {
 };
 // One object of a slab batch with the interface of Ff8EncArgs (rs_ff8.hip: ff8_enc).
 struct Ff8SlabView {
-    uint64_t in_base, in_stride, out_base, out_stride;
+    uint64_t in_base, out_base;
+    int32_t in_stride, out_stride;
     const uint32_t* sktab;
     const uint32_t* fused;
     unsigned K, R, nchunks;
     uint32_t nunits;
     __host__ __device__ Ff8SlabView(const Ff8SlabBatch& b, unsigned o)
-        : in_base(b.in_base[o]), in_stride(b.in_stride[o]), out_base(b.out_base[o]), out_stride(b.out_stride[o]),
+        : in_base(b.in_base[o]), out_base(b.out_base[o]), in_stride(b.in_stride[o]), out_stride(b.out_stride[o]),
           sktab(b.sktab), fused(b.fused), K(b.K), R(b.R), nchunks(b.nchunks), nunits(b.nunits) {}
-    __host__ __device__ uint64_t piece(unsigned i) const {
-        return i < K ? in_base + uint64_t(i) * in_stride : out_base + uint64_t(i - K) * out_stride;
-    }
+    static constexpr bool kSlab = true;  // piece i + 1 = piece i + stride
+    __host__ __device__ uint64_t piece(unsigned i) const { return i < K ? in_piece(i) : out_piece(i - K); }
+    __host__ __device__ uint64_t in_piece(unsigned i) const { return in_base + uint64_t(int64_t(i) * in_stride); }
+    __host__ __device__ uint64_t out_piece(unsigned j) const { return out_base + uint64_t(int64_t(j) * out_stride); }
 };
 struct Ff8DecArgs {
     uint64_t ptr[kFf8Ptrs];        // position p: received piece / output of a lost original / 0

@@ -98,12 +98,16 @@ constexpr int kDefaultEncG = LAMD_FF8_ENC_G;
 // Piece pointers of the NR pieces a lane holds, fetched as one batch of scalar
 // loads: otherwise the compiler sinks each load into the branch that uses it,
 // a chain of dependent scalar-load round trips before the piece loads issue.
-template <int NR, class A, class Idx>
-LDEV void fetch_ptrs(uint64_t (&pp)[NR], const A& a, Idx idx) {
+template <int NR, class Get, class Idx>
+LDEV void fetch_ptrs_by(uint64_t (&pp)[NR], Get get, Idx idx) {
 #pragma unroll
-    for (int r = 0; r < NR; ++r) pp[r] = a.piece(idx(r));
+    for (int r = 0; r < NR; ++r) pp[r] = get(idx(r));
 #pragma unroll
     for (int r = 0; r < NR; ++r) asm volatile("" : "+s"(pp[r]));
+}
+template <int NR, class A, class Idx>
+LDEV void fetch_ptrs(uint64_t (&pp)[NR], const A& a, Idx idx) {
+    fetch_ptrs_by(pp, [&](unsigned i) { return a.piece(i); }, idx);
 }
 
 // This lane's column inside the workgroup's 64-dword strip.  Lanes past the
@@ -137,6 +141,41 @@ LDEV uint32_t gload(uint64_t piece, const Cols& c) {
 }
 LDEV void gstore(uint64_t piece, const Cols& c, uint32_t v) {
     *gptr<uint32_t>(reinterpret_cast<uint8_t*>(piece + c.base) + c.lane_off) = v;
+}
+// p: piece pointer with the strip base already added
+LDEV uint32_t gload_at(uint64_t p, const Cols& c) {
+    return *gptr<const uint32_t>(reinterpret_cast<const uint8_t*>(p) + c.lane_off);
+}
+LDEV void gstore_at(uint64_t p, const Cols& c, uint32_t v) { *gptr<uint32_t>(reinterpret_cast<uint8_t*>(p) + c.lane_off) = v; }
+
+// Strip pointers of the NR consecutive pieces first, first + 1, ... (a lane's
+// registers in layout 0 hold pieces r | w << RB): a slab view steps by its
+// stride (one 64-bit scalar add per piece), a pointer table is read per piece.
+template <int NR, class Get>
+LDEV void run_ptrs(uint64_t (&pp)[NR], Get get, unsigned first, int32_t stride, bool slab, const Cols& c) {
+    if (slab) {
+        uint64_t p = get(first) + c.base;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            pp[r] = p;
+            p += uint64_t(int64_t(stride));
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < NR; ++r) pp[r] = get(first + r) + c.base;
+    }
+#pragma unroll
+    for (int r = 0; r < NR; ++r) asm volatile("" : "+s"(pp[r]));
+}
+template <class A>
+LDEV int32_t in_stride_of(const A& a) {
+    if constexpr (A::kSlab) return a.in_stride;
+    else return 0;
+}
+template <class A>
+LDEV int32_t out_stride_of(const A& a) {
+    if constexpr (A::kSlab) return a.out_stride;
+    else return 0;
 }
 
 // --------------------------------------------------------------- encode -----
@@ -190,23 +229,28 @@ LDEV void ff8_enc(const A& a) {
     const Cols cl = G == 0 ? strip_cols(a.nunits, lane) : strip_cols_lw<LW>(a.nunits, lane);
     const PieceSpace ps{0, 0, 0};
     typename TL::Reg x;
+    // input pieces [0, K) and output pieces [0, R) through their own accessors:
+    // no per-piece select between the two (a slab view's piece(i) compiles to a
+    // dozen scalar instructions per piece, in front of the loads)
+    auto in_ptr = [&](unsigned i) { return a.in_piece(i); };
     auto ptrs = [&](uint64_t (&pp)[TL::NR], auto idx) {
-        if constexpr (G == 0) fetch_ptrs(pp, a, idx);
+        if constexpr (G == 0) fetch_ptrs_by(pp, in_ptr, idx);
         else {
 #pragma unroll
-            for (int r = 0; r < TL::NR; ++r) pp[r] = a.piece(idx(r));  // per lane group
+            for (int r = 0; r < TL::NR; ++r) pp[r] = a.in_piece(idx(r));  // per lane group
         }
     };
     auto load_chunk = [&](unsigned c) {
         const unsigned base = c * m;  // base + tp < nchunks * m <= K + m - 1 < 256
         uint64_t pp[TL::NR];
         if constexpr (G == 0) {
-            ptrs(pp, [&](int r) { return base + TL::piece(0, r, w); });
+            static_assert(TL::lo(0) == 0, "layout 0: register r holds piece r | w << RB");
+            run_ptrs(pp, in_ptr, base + TL::piece(0, 0, w), in_stride_of(a), A::kSlab, cl);
 #pragma unroll
             for (int r = 0; r < TL::NR; ++r) {
                 const unsigned i = base + TL::piece(0, r, w);
-                if constexpr (kDense) x[r][0] = gload(pp[r], cl);
-                else x[r][0] = i < a.K ? gload(pp[r], cl) : 0u;  // past K: zero padding (LeopardFF8.cpp:1631-1634)
+                if constexpr (kDense) x[r][0] = gload_at(pp[r], cl);
+                else x[r][0] = i < a.K ? gload_at(pp[r], cl) : 0u;  // past K: zero padding (LeopardFF8.cpp:1631-1634)
             }
         } else {
             // per-lane pieces: branch-free, padding lanes re-read piece K - 1 and drop it
@@ -270,12 +314,17 @@ LDEV void ff8_enc(const A& a) {
     }
     TL::pin(x);
     uint64_t pp[TL::NR];
-    ptrs(pp, [&](int r) { return a.K + TL::piece(0, r, w); });  // K + tp < K + m <= 256
+    if constexpr (G == 0)
+        run_ptrs(pp, [&](unsigned j) { return a.out_piece(j); }, TL::piece(0, 0, w), out_stride_of(a), A::kSlab, cl);
+    else {
+#pragma unroll
+        for (int r = 0; r < TL::NR; ++r) pp[r] = a.out_piece(TL::piece(0, r, w)) + cl.base;  // tp < m: R + tp < 256
+    }
     if (!cl.live) return;
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) {
         const unsigned tp = TL::piece(0, r, w);
-        if (kDense || tp < a.R) gstore(pp[r], cl, x[r][0]);
+        if (kDense || tp < a.R) gstore_at(pp[r], cl, x[r][0]);
     }
     STAMP(5);
 }

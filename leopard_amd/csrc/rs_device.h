@@ -308,6 +308,15 @@ struct LdsSkew8 {
         return ((j + 1) & j) == 0;
     }
 };
+// The same tables with every butterfly multiplied (a zero skew's all-zero
+// table adds 0).  The XOR-only shortcut is a wave-uniform branch per group; in
+// straight-line tiles (the GF(2^8) dense forms) its two paths cost register
+// copies at every merge (~110 v_mov per wave in the 16-pieces-per-lane batch
+// tile), more than the multiplies it saves, which are concentrated in the
+// waves holding the first positions (the others run every multiply anyway).
+struct LdsSkew8NoZero : LdsSkew8 {
+    LDEV constexpr bool zero(unsigned) const { return false; }
+};
 template <class F>
 struct GlobalWindow {
     const uint32_t* sk = nullptr;

@@ -90,6 +90,9 @@ constexpr uint32_t kOneWgPerCuUnits = 256 * 64;  // 256 CUs x one 64-dword strip
 // 11.5, G = 2 11.9 (per-workgroup table staging and per-lane-group table reads
 // outweigh the phase overlap; profiles/r01_v7/lane_groups_ab.txt), so the
 // default stays 0 and LEO_AMD_FF8_G selects the others for experiments.
+#ifndef LAMD_DENSE_ZERO_CHECK
+#define LAMD_DENSE_ZERO_CHECK 0
+#endif
 #ifndef LAMD_FF8_ENC_G
 #define LAMD_FF8_ENC_G 0
 #endif
@@ -284,11 +287,16 @@ LDEV void ff8_enc(const A& a) {
     LdsSkew8 win{tabs};
     if constexpr (kDense) {
         // encode: IFFT skew base m - 1, FFT base -1; inverse: the other way round
-        win.stage(nullptr, kForm == kFormDenseDec ? -1 : int(m - 1));
-        ifft(win, AllLive{});
+#if LAMD_DENSE_ZERO_CHECK
+        LdsSkew8 dwin{tabs};  // experiments: the XOR-only shortcut of zero skews
+#else
+        LdsSkew8NoZero dwin{{tabs}};
+#endif
+        dwin.stage(nullptr, kForm == kFormDenseDec ? -1 : int(m - 1));
+        ifft(dwin, AllLive{});
         TL::fused_top(x, FF8::tab_at(a.fused));
-        win.stage(nullptr, kForm == kFormDenseDec ? int(m - 1) : -1);
-        fft(win, AllLive{});
+        dwin.stage(nullptr, kForm == kFormDenseDec ? int(m - 1) : -1);
+        fft(dwin, AllLive{});
     } else if constexpr (!kMulti) {
         win.stage(nullptr, int(m - 1));
         ifft(win, lane_pred<G>(BelowLive{a.K}));

@@ -174,6 +174,8 @@ struct PieceMap {
     uint8_t* base;
     uint64_t stride;
     uint64_t off;
+    // a map known to be a slab (the multi-pass intermediates): no table test
+    LDEV uint8_t* slab_ptr(unsigned i) const { return base + uint64_t(i) * stride + off; }
     LDEV uint8_t* ptr(unsigned i) const {
         uint8_t* p = table ? reinterpret_cast<uint8_t*>(cload64(table + i)) : base + uint64_t(i) * stride;
         return p + off;

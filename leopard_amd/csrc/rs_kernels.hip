@@ -94,6 +94,39 @@ LDEV void ld16z(uint32_t* x, const PieceMap& pm, bool ok, unsigned i, const uint
     ld16(x, base, c.off);
 }
 
+// Strip addresses of the pieces of a caller's piece map (a pointer table or a
+// slab, wave-uniform) that a lane's registers r < NR hold, `ok(r)` false: the
+// zero page.  The table-or-slab test is made once for all of them, the table
+// entries are read back to back (one scalar-load round trip instead of one per
+// piece) and the zero-page choice is a select, not a branch: per piece the
+// prologue is a few scalar instructions, not a dozen and three branches.
+template <int NR, class Idx, class Ok>
+LDEV void map_ptrs(const uint8_t* (&pp)[NR], const PieceMap& pm, Idx idx, Ok ok, const uint8_t* zeros,
+                   const Cols16& c) {
+    uint64_t q[NR];
+    if (pm.table) {
+#pragma unroll
+        for (int r = 0; r < NR; ++r) q[r] = cload64(pm.table + (ok(r) ? idx(r) : 0u));  // entry 0 always exists
+    } else {
+#pragma unroll
+        for (int r = 0; r < NR; ++r) q[r] = uint64_t(reinterpret_cast<uintptr_t>(pm.base)) + uint64_t(idx(r)) * pm.stride;
+    }
+#pragma unroll
+    for (int r = 0; r < NR; ++r) pp[r] = ok(r) ? reinterpret_cast<const uint8_t*>(q[r] + pm.off + c.strip) : zeros;
+}
+// x[r] <- the pieces of a caller's map for r < NR (map_ptrs), in batches of 8
+template <class TL, class Idx, class Ok>
+LDEV void load_map(typename TL::Reg& x, const PieceMap& pm, Idx idx, Ok ok, const uint8_t* zeros, const Cols16& c) {
+    constexpr int B = TL::NR < 8 ? TL::NR : 8;
+    static_for<0, TL::NR / B>([&](auto BI) {
+        constexpr int r0 = decltype(BI)::value * B;
+        const uint8_t* pp[B];
+        map_ptrs(pp, pm, [&](int r) { return idx(r0 + r); }, [&](int r) { return ok(r0 + r); }, zeros, c);
+#pragma unroll
+        for (int r = 0; r < B; ++r) ld16(x[r0 + r], pp[r], c.off);
+    });
+}
+
 // Piece i of pm when `ok` (wave-uniform), else zeros read from the zero page.
 // The choice is made on scalars so the vector code has no branch.
 template <class F>
@@ -215,7 +248,8 @@ LDEV void xor_load(typename TL::Reg& x, const PieceMap& pm, PosFn pos, unsigned 
     static_for<0, TL::NR / B>([&](auto BI) {
         constexpr int r0 = decltype(BI)::value * B;
         uint32_t y[B][TL::U];
-        static_for<0, B>([&](auto I) { ld16(y[I.value], pm.ptr(pos(TL::piece(LAY, r0 + I.value, w))) + cl.strip, cl.off); });
+        static_for<0, B>([&](auto I) { ld16(y[I.value], pm.slab_ptr(pos(TL::piece(LAY, r0 + I.value, w))) + cl.strip, cl.off); });
+        __builtin_amdgcn_sched_barrier(0);  // one batch of loads in flight at a time
         static_for<0, B>([&](auto I) {
 #pragma unroll
             for (int k = 0; k < TL::U; ++k) x[r0 + I.value][k] ^= y[I.value][k];
@@ -241,11 +275,8 @@ __global__ void __launch_bounds__(threads16(kLoBits, R), 4) k_enc_lo(EncArgs a) 
     Tabs16Stage<NT, T> st;
     st.load(a.sktab, int(m - 1 + base), y << T, 0);
     typename TL::Reg x;
-#pragma unroll
-    for (int r = 0; r < TL::NR; ++r) {
-        const unsigned g = ps.global(TL::piece(0, r, w));
-        ld16z(x[r], a.in, base + g < a.K, base + g, a.zeros, cl);
-    }
+    load_map<TL>(x, a.in, [&](int r) { return base + ps.global(TL::piece(0, r, w)); },
+                 [&](int r) { return base + ps.global(TL::piece(0, r, w)) < a.K; }, a.zeros, cl);
     st.store(set);
     __syncthreads();
     TL::ifft(x, w, lane, lds, ps, LdsWindow16{set, y << T, 0}, prune16(BelowLive{a.K - base}));
@@ -253,7 +284,7 @@ __global__ void __launch_bounds__(threads16(kLoBits, R), 4) k_enc_lo(EncArgs a) 
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) {
         const unsigned g = ps.global(TL::piece(TL::kLast, r, w));
-        st16(a.slab_out.ptr(base + g) + cl.strip, cl.off, x[r]);
+        st16(a.slab_out.slab_ptr(base + g) + cl.strip, cl.off, x[r]);
     }
 }
 
@@ -281,7 +312,8 @@ __global__ void __launch_bounds__(threads16(T, R), LAMD_HI_WAVES) k_enc_hi(EncAr
         for (int r = 0; r < TL::NR; ++r) {
             const unsigned tp = TL::piece(0, r, w);
             // low tiles that lie entirely past K were all-zero inputs
-            ld16z(x[r], a.slab_in, base + (tp << kLoBits) < a.K, base + ps.global(tp), a.zeros, cl);
+            const bool ok = base + (tp << kLoBits) < a.K;
+            ld16(x[r], ok ? a.slab_in.slab_ptr(base + ps.global(tp)) + cl.strip : a.zeros, cl.off);
         }
     };
     {
@@ -318,7 +350,7 @@ __global__ void __launch_bounds__(threads16(T, R), LAMD_HI_WAVES) k_enc_hi(EncAr
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) {
         const unsigned g = ps.global(TL::piece(0, r, w));
-        st16(a.slab_out.ptr(g) + cl.strip, cl.off, x[r]);
+        st16(a.slab_out.slab_ptr(g) + cl.strip, cl.off, x[r]);
     }
 }
 
@@ -341,7 +373,7 @@ __global__ void __launch_bounds__(threads16(kLoBits, R), 4) k_enc_fin(EncArgs a)
     typename TL::Reg x;
     auto pos = [&](unsigned tp) { return ps.global(tp); };
 #pragma unroll
-    for (int r = 0; r < TL::NR; ++r) ld16(x[r], a.slab_in.ptr(pos(TL::piece(TL::kLast, r, w))) + cl.strip, cl.off);
+    for (int r = 0; r < TL::NR; ++r) ld16(x[r], a.slab_in.slab_ptr(pos(TL::piece(TL::kLast, r, w))) + cl.strip, cl.off);
     st.store(set);
     __syncthreads();
     if (a.Tm == unsigned(kLoBits))
@@ -355,7 +387,6 @@ __global__ void __launch_bounds__(threads16(kLoBits, R), 4) k_enc_fin(EncArgs a)
         if (g < a.R) st16(a.out.ptr(g) + cl.strip, cl.off, x[r]);
     }
 }
-
 // ------------------------------------------------------------------ decode --
 
 LDEV bool bit_set(const uint32_t* bits, unsigned p) { return (cload(bits + (p >> 5)) >> (p & 31)) & 1u; }
@@ -421,7 +452,7 @@ __global__ void __launch_bounds__(threads16(kLoBits, R), 4) k_dec_lo(DecArgs a) 
     TL::ifft(v, w, lane, lds, ps, LdsWindow16{set, y << T, 0}, prune16(Pyr16Live{a.present_pyr}));
     if (!live) return;
 #pragma unroll
-    for (int r = 0; r < TL::NR; ++r) st16(a.a_out.ptr(ps.global(TL::piece(TL::kLast, r, w))) + cl.strip, cl.off, v[r]);
+    for (int r = 0; r < TL::NR; ++r) st16(a.a_out.slab_ptr(ps.global(TL::piece(TL::kLast, r, w))) + cl.strip, cl.off, v[r]);
 }
 
 // pass 2: A = F_hi (I + D_hi) I_hi U over the high bits, computed as
@@ -444,7 +475,7 @@ __global__ void __launch_bounds__(threads16(T, R), LAMD_HI_WAVES) k_dec_hi(DecAr
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) {
         const unsigned tp = TL::piece(0, r, w);
-        ld16z(v[r], a.a_in, tp < a.nlo, ps.global(tp), a.zeros, cl);
+        ld16(v[r], tp < a.nlo ? a.a_in.slab_ptr(ps.global(tp)) + cl.strip : a.zeros, cl.off);
     }
     st.store(set);
     __syncthreads();
@@ -458,7 +489,7 @@ __global__ void __launch_bounds__(threads16(T, R), LAMD_HI_WAVES) k_dec_hi(DecAr
 #pragma unroll
         for (int r = 0; r < TL::NR; ++r) {
             const unsigned p = ps.global(TL::piece(0, r, w));
-            if (needed(p, kLoBits)) st16(a.a_out.ptr(p) + cl.strip, cl.off, v[r]);
+            if (needed(p, kLoBits)) st16(a.a_out.slab_ptr(p) + cl.strip, cl.off, v[r]);
         }
 }
 
@@ -486,7 +517,7 @@ __global__ void __launch_bounds__(threads16(T, R), LAMD_HI_WAVES) k_dec_hi_half(
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) {
         const unsigned tp = TL::piece(0, r, w);
-        ld16z(v[r], a.a_in, tp < a.nlo, low.global(tp), a.zeros, cl);
+        ld16(v[r], tp < a.nlo ? a.a_in.slab_ptr(low.global(tp)) + cl.strip : a.zeros, cl.off);
     }
     sl.store(lset);
     sh.store(hset);
@@ -496,7 +527,7 @@ __global__ void __launch_bounds__(threads16(T, R), LAMD_HI_WAVES) k_dec_hi_half(
     TL::template fft<true>(v, w, lane, lds, high, LdsWindow16{hset, a.m, kLoBits}, prune16(Pyr16Live{a.needed_pyr}));
     if (live)
 #pragma unroll
-        for (int r = 0; r < TL::NR; ++r) st16(a.a_out.ptr(high.global(TL::piece(0, r, w))) + cl.strip, cl.off, v[r]);
+        for (int r = 0; r < TL::NR; ++r) st16(a.a_out.slab_ptr(high.global(TL::piece(0, r, w))) + cl.strip, cl.off, v[r]);
 }
 
 // pass 3: z = A + D_lo(U), FFT over the low bits, reveal lost originals
@@ -524,14 +555,14 @@ __global__ void __launch_bounds__(threads16(kLoBits, R), 4) k_dec_fin(DecArgs a)
     ls.load(a.tabs, a.reveal_logs + (y << T));
     typename TL::Reg z;
 #pragma unroll
-    for (int r = 0; r < TL::NR; ++r) ld16(z[r], a.a_in.ptr(ps.global(TL::piece(TL::kLast, r, w))) + cl.strip, cl.off);
+    for (int r = 0; r < TL::NR; ++r) ld16(z[r], a.a_in.slab_ptr(ps.global(TL::piece(TL::kLast, r, w))) + cl.strip, cl.off);
     st.store(set);
     ls.store(rvl);
     __syncthreads();
     // U of a tile past the received ones is zero, and so is D_lo(U) (workgroup-uniform)
     if (y < a.nlo)
         TL::derivative_add(z, [&](int r, uint32_t* out) {
-            ld16(out, a.b_in.ptr(ps.global(TL::piece(TL::kLast, r, w))) + cl.strip, cl.off);
+            ld16(out, a.b_in.slab_ptr(ps.global(TL::piece(TL::kLast, r, w))) + cl.strip, cl.off);
         }, w, lane, lds);
     TL::fft(z, w, lane, lds, ps, LdsWindow16{set, y << T, 0}, prune16(Pyr16Live{a.needed_pyr}));
     if (!live) return;

@@ -93,6 +93,16 @@ constexpr uint32_t kOneWgPerCuUnits = 256 * 64;  // 256 CUs x one 64-dword strip
 #ifndef LAMD_DENSE_ZERO_CHECK
 #define LAMD_DENSE_ZERO_CHECK 0
 #endif
+// Window of the pruned (non-dense) tiles: LAMD_FF8_ZERO_CHECK=1 keeps the
+// XOR-only branch for zero skews (rs_device.h: LdsSkew8NoZero)
+#ifndef LAMD_FF8_ZERO_CHECK
+#define LAMD_FF8_ZERO_CHECK 0
+#endif
+#if LAMD_FF8_ZERO_CHECK
+struct Skew8Win : LdsSkew8 {};
+#else
+using Skew8Win = LdsSkew8NoZero;
+#endif
 #ifndef LAMD_FF8_ENC_G
 #define LAMD_FF8_ENC_G 0
 #endif
@@ -284,7 +294,7 @@ LDEV void ff8_enc(const A& a) {
     stage.store(tabs);
     __syncthreads();
     STAMP(2);
-    LdsSkew8 win{tabs};
+    Skew8Win win{{tabs}};
     if constexpr (kDense) {
         // encode: IFFT skew base m - 1, FFT base -1; inverse: the other way round
 #if LAMD_DENSE_ZERO_CHECK
@@ -413,7 +423,7 @@ LDEV void ff8_dec(const Ff8DecArgs& a) {
     STAMP(2);
     // scale by exp(el) (absent pieces stay zero)
     scale_batched<TL>(v, ltab, [&](int r) { return el_at(a, pos(r)); }, [&](int r) { return present(pos(r), 0); });
-    LdsSkew8 win{sk};
+    Skew8Win win{{sk}};
     win.stage(nullptr, -1);
     // IFFT and FFT without their top layers around swap_top + D_low (see
     // Tile::derivative_swaptop): the same map as IFFT, (I + D), FFT
@@ -499,7 +509,7 @@ LDEV void ff8_dec_half(const Ff8DecArgs& a) {
     log_stage.store(ltab);
     __syncthreads();
     scale_batched<TL>(v, ltab, [&](int r) { return el_at(a, lpos(r)); }, [&](int r) { return present(lpos(r), 0); });
-    LdsSkew8 win{sk};
+    Skew8Win win{{sk}};
     win.stage(nullptr, -1);  // decoder skew base (LeopardFF8.cpp:1880, 1903)
     // both top layers (single skews m/2 - 1 and m + m/2 - 1) as one butterfly
     // with their sum, the encoder's chunk-0 fused table (Tile::fused_top)
@@ -568,7 +578,7 @@ LDEV void ff8_dec_split(const Ff8DecArgs& a) {
     sk_stage.store(sk);
     log_stage.store(ltab);
     __syncthreads();
-    LdsSkew8 win{sk};
+    Skew8Win win{{sk}};
     win.stage(nullptr, -1);  // decoder skew base (LeopardFF8.cpp:1880, 1903)
     // y = N(I_H(h * exp(el)))
     scale_batched<TL>(h, ltab, [&](int r) { return el_at(a, hpos(r)); }, [&](int r) { return present(hpos(r), 0); });

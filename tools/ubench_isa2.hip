@@ -33,6 +33,13 @@ __global__ void __launch_bounds__(256) k(uint32_t* out, int iters, uint32_t s) {
                 if constexpr (OP == 8) asm volatile("v_lshl_or_b32 %0, %1, 3, %0" : "+v"(v[i]) : "v"(w[i]));
                 if constexpr (OP == 9) asm volatile("v_pk_add_u16 %0, %1, %0" : "+v"(v[i]) : "v"(w[i]));
                 if constexpr (OP == 10) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(v[i]) : "v"(w[i]));
+                if constexpr (OP == 11) {  // one 64-bit shift of a register pair (the pair counts as one instruction)
+                    uint64_t p = (uint64_t(w[i]) << 32) | v[i];
+                    asm volatile("v_lshrrev_b64 %0, 3, %0" : "+v"(p));
+                    v[i] = uint32_t(p);
+                    w[i] = uint32_t(p >> 32);
+                }
+                if constexpr (OP == 12) asm volatile("v_alignbit_b32 %0, %0, %1, 3" : "+v"(v[i]) : "v"(w[i]));
             }
         }
     }
@@ -83,5 +90,7 @@ int main() {
     run<9>(out, "v_pk_add_u16");
     run<10>(out, "v_cndmask_b32");
     run<0>(out, "perm+and+xor (compiled)");
+    run<11>(out, "v_lshrrev_b64");
+    run<12>(out, "v_alignbit_b32");
     return 0;
 }

@@ -90,6 +90,9 @@ constexpr uint32_t kOneWgPerCuUnits = 256 * 64;  // 256 CUs x one 64-dword strip
 // 11.5, G = 2 11.9 (per-workgroup table staging and per-lane-group table reads
 // outweigh the phase overlap; profiles/r01_v7/lane_groups_ab.txt), so the
 // default stays 0 and LEO_AMD_FF8_G selects the others for experiments.
+#ifndef LAMD_PRIO_LOADS
+#define LAMD_PRIO_LOADS 0
+#endif
 #ifndef LAMD_DENSE_ZERO_CHECK
 #define LAMD_DENSE_ZERO_CHECK 0
 #endif
@@ -289,7 +292,13 @@ LDEV void ff8_enc(const A& a) {
         if constexpr (pipe8(NA)) TL::template fft_pl<true>(x, w, lane, ring, ps, win, pred);
         else TL::template fft<true>(x, w, lane, lds, ps, win, pred);
     };
+#if LAMD_PRIO_LOADS
+    __builtin_amdgcn_s_setprio(3);  // experiments: issue this workgroup's loads ahead of other waves' butterflies
+#endif
     load_chunk(0);
+#if LAMD_PRIO_LOADS
+    __builtin_amdgcn_s_setprio(0);
+#endif
     STAMP(1);
     stage.store(tabs);
     __syncthreads();

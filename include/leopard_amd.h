@@ -19,6 +19,16 @@ extern "C" {
  * Per thread. */
 LEO_EXPORT void leo_amd_set_stream(void* hip_stream);
 
+/* Scratch: the library keeps per (calling thread, device, stream) scratch --
+ * a device arena, pinned staging, and for host-memory calls a pinned ring with
+ * two streams -- and keeps at most 8 of them per thread (least recently used
+ * freed first).  A thread's scratch is freed when the thread exits.  This call
+ * frees the calling thread's scratch for `hip_stream` on every device, after
+ * the work this library queued on that stream has finished; call it before
+ * destroying a stream used with leo_amd_set_stream.  (void*)-1 frees the
+ * calling thread's scratch of every stream. */
+LEO_EXPORT void leo_amd_release_stream(void* hip_stream);
+
 /* 1: device-resident calls return after enqueueing work on the stream (the
  * caller orders later reads on that stream).  0 (default): every call
  * synchronises, like the reference.  Host-memory calls are always synchronous.

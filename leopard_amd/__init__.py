@@ -34,7 +34,7 @@ LEO_VERSION = 2
 __all__ = [
     "LEO_VERSION", "LeopardResult", "leo_init", "leo_result_string", "leo_encode_work_count", "leo_encode",
     "leo_decode_work_count", "leo_decode", "leo_amd_encode_slice", "leo_amd_decode_slice", "leo_amd_encode_batch",
-    "leo_amd_decode_batch", "register_host", "unregister_host", "set_fanout", "set_stream",
+    "leo_amd_decode_batch", "register_host", "unregister_host", "set_fanout", "set_stream", "release_stream",
     "set_async", "set_device", "device_count", "table", "last_error", "encode", "decode", "LIB_PATH", "lib",
 ]
 
@@ -78,6 +78,7 @@ def _load():
         "leo_amd_set_async": (None, [i]),
         "leo_amd_set_device": (None, [i]),
         "leo_amd_set_fanout": (None, [i]),
+        "leo_amd_release_stream": (None, [vp]),
         "leo_amd_device_count": (i, []),
         "leo_amd_table": (i, [i, i, vp, u]),
         "leo_amd_last_error": (ctypes.c_char_p, []),
@@ -152,16 +153,27 @@ def _ptr_arrays(seqs):
     return outer
 
 
+def _batch_lists(**lists):
+    """Every per-object list of a batch call must name the same objects: the C
+    side reads object_count entries of each outer array."""
+    counts = {name: len(v) for name, v in lists.items()}
+    if len(set(counts.values())) != 1:
+        raise ValueError(f"batch lists differ in length: {counts}")
+    return next(iter(counts.values()))
+
+
 def leo_amd_encode_batch(buffer_bytes, original_count, recovery_count, work_count, original_data,
                          work_data) -> LeopardResult:
     """original_data / work_data: one pointer sequence per object (include/leopard_amd.h)."""
-    return LeopardResult(lib.leo_amd_encode_batch(len(original_data), buffer_bytes, original_count, recovery_count,
+    count = _batch_lists(original_data=original_data, work_data=work_data)
+    return LeopardResult(lib.leo_amd_encode_batch(count, buffer_bytes, original_count, recovery_count,
                                                   work_count, _ptr_arrays(original_data), _ptr_arrays(work_data)))
 
 
 def leo_amd_decode_batch(buffer_bytes, original_count, recovery_count, work_count, original_data, recovery_data,
                          work_data) -> LeopardResult:
-    return LeopardResult(lib.leo_amd_decode_batch(len(original_data), buffer_bytes, original_count, recovery_count,
+    count = _batch_lists(original_data=original_data, recovery_data=recovery_data, work_data=work_data)
+    return LeopardResult(lib.leo_amd_decode_batch(count, buffer_bytes, original_count, recovery_count,
                                                   work_count, _ptr_arrays(original_data), _ptr_arrays(recovery_data),
                                                   _ptr_arrays(work_data)))
 
@@ -178,6 +190,12 @@ def unregister_host(ptr: int) -> LeopardResult:
 def set_stream(stream_handle: Optional[int]) -> None:
     """HIP stream (integer handle, e.g. torch.cuda.current_stream().cuda_stream) for this thread."""
     lib.leo_amd_set_stream(None if not stream_handle else ctypes.c_void_p(stream_handle))
+
+
+def release_stream(stream_handle: Optional[int]) -> None:
+    """Free this thread's library scratch for a HIP stream (-1: every stream), after
+    the work the library queued on it; call before destroying the stream."""
+    lib.leo_amd_release_stream(None if not stream_handle else ctypes.c_void_p(stream_handle))
 
 
 def set_async(enable: bool) -> None:

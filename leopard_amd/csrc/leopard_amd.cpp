@@ -47,6 +47,20 @@ void set_error(const char* what, hipError_t e) {
     tls.last_error = buf;
 }
 
+// A/B switches of the performance experiments (tools/): read from the
+// environment only in builds with LAMD_EXPERIMENT_ENV=1.  The shipped library
+// (Makefile default) ignores them and always takes the default paths, which
+// are the ones the tests cover.
+bool experiment_off(const char* name) {
+#if LAMD_EXPERIMENT_ENV
+    const char* e = std::getenv(name);
+    return e && e[0] == '0';
+#else
+    (void)name;
+    return false;
+#endif
+}
+
 #define HIP_OK(expr, what)                         \
     do {                                           \
         hipError_t e_ = (expr);                    \
@@ -68,6 +82,7 @@ struct DeviceTables {
     uint32_t* walsh8 = nullptr;
     uint32_t* walsh16 = nullptr;
     uint8_t* zeros = nullptr;   // zero page
+    hipStream_t svc = nullptr;  // library-owned stream for releasing workspace memory
     bool ready = false;
 };
 
@@ -102,22 +117,69 @@ LeopardResult ensure_device(int dev, DeviceTables** out) {
         HIP_OK(upload(&d.walsh16, g_h_walsh16), "upload FF16 LogWalsh");
         HIP_OK(hipMalloc(reinterpret_cast<void**>(&d.zeros), 4096), "zero page");
         HIP_OK(hipMemset(d.zeros, 0, 4096), "zero page");
+        HIP_OK(hipStreamCreateWithFlags(&d.svc, hipStreamNonBlocking), "service stream");
         d.ready = true;
     }
     *out = &d;
     return Leopard_Success;
 }
 
-// Scratch of one (thread, device, stream): device arena (grow-only) plus a
-// pinned host staging area for pointer tables / bitmaps.  Keyed by stream as
-// well as by device: the kernels of a call read the arena after the call
-// returns (async mode), and only calls on the same stream are ordered after
-// them, so two streams must never share one arena.
+// Set by an atexit handler (registered in leo_init after the HIP runtime is
+// up, so it runs before the runtime's own teardown): workspaces destroyed
+// after it leave their memory to process teardown instead of calling into a
+// runtime that may be half gone.
+std::atomic<bool> g_exiting{false};
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        (void)hipGetDevice(&prev);
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        (void)hipGetDevice(&cur);
+        if (prev >= 0 && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+// Frees stream-ordered allocations that nothing uses any more on the device's
+// service stream and trims the default pool, so that the memory is free again
+// (hipMemGetInfo) when this returns.
+void release_device_memory(int dev, std::initializer_list<void*> ptrs) {
+    hipStream_t svc = dev >= 0 && dev < int(g_dev.size()) ? g_dev[dev].svc : nullptr;
+    bool any = false;
+    for (void* p : ptrs)
+        if (p) {
+            (void)hipFreeAsync(p, svc);
+            any = true;
+        }
+    if (!any) return;
+    (void)hipStreamSynchronize(svc);
+    hipMemPool_t pool = nullptr;
+    if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess && pool) (void)hipMemPoolTrimTo(pool, 0);
+}
+
+// Scratch of one (thread, device, stream): device arena plus a pinned host
+// staging area for pointer tables / bitmaps.  Keyed by stream as well as by
+// device: the kernels of a call read the arena after the call returns (async
+// mode), and only calls on the same stream are ordered after them, so two
+// streams must never share one arena.
+//
+// Lifetime: a thread keeps at most kMaxWorkspaces of them (least recently used
+// evicted first) and releases all of them when it exits.  Device memory is
+// allocated and freed stream-ordered on the workspace's stream (growth never
+// synchronises the device), and `last_use` -- recorded on the stream after
+// every call that used the workspace's memory -- is waited for before a
+// workspace is freed, so release is safe even after the caller destroyed the
+// stream.  (The reference holds no per-call state at all)
 struct Workspace {
     int dev = -1;
     hipStream_t stream = nullptr;
     uint8_t* dbuf = nullptr;
     size_t dsize = 0;
+    hipEvent_t last_use = nullptr;
+    bool touched = false;  // the current call enqueued work that uses this workspace's memory
     // Pinned staging ring for small host->device uploads (pointer tables,
     // batch argument blocks, decoder state): a slot is rewritten only after
     // the copy issued from it kBack uploads ago has completed, so back-to-back
@@ -149,8 +211,42 @@ struct Workspace {
     uint8_t* dec16 = nullptr;
     std::vector<uint32_t> dec16_key;
 
-    ~Workspace() {
-        // Process teardown: the runtime may already be gone; leak rather than crash.
+    ~Workspace() { release(); }
+    // Waits for the work that may still use this workspace, then frees it.
+    void release() {
+        if (g_exiting.load()) return;  // process teardown: the runtime may already be gone
+        DeviceGuard guard(dev);
+        if (last_use) (void)hipEventSynchronize(last_use);
+        for (int s = 0; s < 2; ++s)
+            if (pipe_stream[s]) (void)hipStreamSynchronize(pipe_stream[s]);
+        for (StageSlot& sl : stage) {
+            if (sl.pending) (void)hipEventSynchronize(sl.done);
+            if (sl.host) (void)hipHostFree(sl.host);
+            if (sl.done) (void)hipEventDestroy(sl.done);
+            sl = StageSlot{};
+        }
+        release_device_memory(dev, {dbuf, dec16, ring_dev});
+        if (ring_host) (void)hipHostFree(ring_host);
+        for (int s = 0; s < 2; ++s) {
+            if (pipe_stream[s]) (void)hipStreamDestroy(pipe_stream[s]);
+            if (in_done[s]) (void)hipEventDestroy(in_done[s]);
+            if (out_done[s]) (void)hipEventDestroy(out_done[s]);
+            pipe_stream[s] = nullptr;
+            in_done[s] = out_done[s] = nullptr;
+        }
+        if (last_use) (void)hipEventDestroy(last_use);
+        dbuf = dec16 = ring_dev = ring_host = ring_host_dev = nullptr;
+        last_use = nullptr;
+        dsize = slot_bytes = 0;
+    }
+    // Called at the end of every call: marks where the work of this call that
+    // uses the workspace's memory ends on the stream.
+    LeopardResult mark_use(hipStream_t s) {
+        if (!touched) return Leopard_Success;
+        touched = false;
+        if (!last_use) HIP_OK(hipEventCreateWithFlags(&last_use, hipEventDisableTiming), "event");
+        HIP_OK(hipEventRecord(last_use, s), "record workspace use");
+        return Leopard_Success;
     }
     LeopardResult reserve_ring(size_t bytes_per_slot) {
         for (int s = 0; s < 2; ++s) {
@@ -160,28 +256,34 @@ struct Workspace {
         }
         if (bytes_per_slot <= slot_bytes) return Leopard_Success;
         if (ring_dev) {
-            HIP_OK(hipDeviceSynchronize(), "sync before ring growth");
-            HIP_OK(hipFree(ring_dev), "free ring");
+            // the ring is used only by its own two streams (the host pipeline
+            // waits for both before returning, so this is normally a no-op)
+            for (int s = 0; s < 2; ++s) HIP_OK(hipStreamSynchronize(pipe_stream[s]), "sync before ring growth");
+            HIP_OK(hipFreeAsync(ring_dev, pipe_stream[0]), "free ring");
             HIP_OK(hipHostFree(ring_host), "free pinned ring");
             ring_dev = ring_host = ring_host_dev = nullptr;
             slot_bytes = 0;
         }
         const size_t want = (bytes_per_slot + 4095) / 4096 * 4096;
-        HIP_OK(hipMalloc(reinterpret_cast<void**>(&ring_dev), 2 * want), "allocate device ring");
+        HIP_OK(hipMallocAsync(reinterpret_cast<void**>(&ring_dev), 2 * want, pipe_stream[0]), "allocate device ring");
+        // both pipe streams use it: the second one waits for the allocation
+        HIP_OK(hipEventRecord(in_done[0], pipe_stream[0]), "record ring allocation");
+        HIP_OK(hipStreamWaitEvent(pipe_stream[1], in_done[0], 0), "order ring allocation");
         HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&ring_host), 2 * want, hipHostMallocDefault), "pinned ring");
         HIP_OK(hipHostGetDevicePointer(reinterpret_cast<void**>(&ring_host_dev), ring_host, 0), "map pinned ring");
         slot_bytes = want;
         return Leopard_Success;
     }
+    // Device arena of at least `bytes`, stream-ordered: a grown arena replaces
+    // the old one after this stream's earlier work (no device synchronisation).
     LeopardResult reserve_device(size_t bytes) {
+        touched = true;
         if (bytes <= dsize) return Leopard_Success;
-        if (dbuf) {
-            HIP_OK(hipDeviceSynchronize(), "sync before scratch growth");
-            HIP_OK(hipFree(dbuf), "free scratch");
-            dbuf = nullptr;
-        }
-        size_t want = std::max(bytes, dsize * 2);
-        HIP_OK(hipMalloc(reinterpret_cast<void**>(&dbuf), want), "allocate scratch");
+        const size_t want = std::max(bytes, dsize * 2);
+        if (dbuf) HIP_OK(hipFreeAsync(dbuf, stream), "free scratch");
+        dbuf = nullptr;
+        dsize = 0;
+        HIP_OK(hipMallocAsync(reinterpret_cast<void**>(&dbuf), want, stream), "allocate scratch");
         dsize = want;
         return Leopard_Success;
     }
@@ -190,6 +292,7 @@ struct Workspace {
     // ordered on stream s.
     template <class Fill>
     LeopardResult upload(void* dst, size_t bytes, hipStream_t s, Fill&& fill) {
+        touched = true;
         StageSlot& sl = stage[stage_next];
         stage_next = (stage_next + 1) % kStageSlots;
         if (sl.pending) {
@@ -214,15 +317,55 @@ struct Workspace {
         return upload(dst, bytes, s, [&](uint8_t* h) { std::memcpy(h, src, bytes); });
     }
 };
-thread_local std::vector<std::unique_ptr<Workspace>> tws;
+// The calling thread's workspaces, most recently used first; released when the
+// thread exits.  At most kMaxWorkspaces are kept: one API call uses at most
+// three (its own and the host pipeline's two slot streams), always the most
+// recently used ones, so eviction never frees one that a call in progress holds.
+constexpr size_t kMaxWorkspaces = 8;
+struct WorkspaceList {
+    std::vector<std::unique_ptr<Workspace>> list;
+    ~WorkspaceList() { list.clear(); }
+};
+thread_local WorkspaceList tws;
+
+// Frees workspace i (waiting for its work) and the workspaces of the host
+// pipeline streams it owned (those streams are destroyed with it).
+void drop_workspace(size_t i) {
+    auto& l = tws.list;
+    const hipStream_t ps[2] = {l[i]->pipe_stream[0], l[i]->pipe_stream[1]};
+    l.erase(l.begin() + i);
+    for (hipStream_t p : ps)
+        for (size_t j = 0; p && j < l.size();)
+            if (l[j]->stream == p) l.erase(l.begin() + j);
+            else ++j;
+}
 
 Workspace& workspace(int dev, hipStream_t stream) {
-    for (auto& w : tws)
-        if (w->dev == dev && w->stream == stream) return *w;
-    tws.push_back(std::make_unique<Workspace>());
-    tws.back()->dev = dev;
-    tws.back()->stream = stream;
-    return *tws.back();
+    auto& l = tws.list;
+    for (size_t i = 0; i < l.size(); ++i)
+        if (l[i]->dev == dev && l[i]->stream == stream) {
+            std::rotate(l.begin(), l.begin() + i, l.begin() + i + 1);
+            return *l.front();
+        }
+    l.insert(l.begin(), std::make_unique<Workspace>());
+    l.front()->dev = dev;
+    l.front()->stream = stream;
+    while (l.size() > kMaxWorkspaces) drop_workspace(l.size() - 1);  // least recently used
+    return *l.front();
+}
+
+// Drops the calling thread's workspaces of `stream` (every device), or all of
+// them (leo_amd_release_stream).
+void release_workspaces(hipStream_t stream, bool all) {
+    auto& l = tws.list;
+    for (size_t i = 0; i < l.size();) {
+        if (all || l[i]->stream == stream) {
+            drop_workspace(i);  // may remove entries before i as well
+            i = 0;
+        } else {
+            ++i;
+        }
+    }
 }
 
 // ------------------------------------------------------------ call helpers --
@@ -344,6 +487,10 @@ LeopardResult begin_call(int dev, Call& c) {
 
 LeopardResult finish(const Call& c, bool force_sync) {
     HIP_OK(hipGetLastError(), "kernel launch");
+    if (c.ws) {
+        const LeopardResult r = c.ws->mark_use(c.s);
+        if (r != Leopard_Success) return r;
+    }
     if (force_sync || !tls.async) HIP_OK(hipStreamSynchronize(c.s), "stream synchronize");
     return Leopard_Success;
 }
@@ -467,43 +614,16 @@ LeopardResult xor_device(Call& c, uint64_t bytes, uint64_t off, const void* cons
 
 // --------------------------------------------------------------- decode ----
 
-// FF8 error locator on the host (n <= 256 positions, a few thousand integer ops):
-// el = FWHT(LogWalsh * FWHT(erasures)) mod 255 (LeopardFF8.cpp:1848-1853).  The
-// last pattern is cached per thread (repeated erasure patterns are common).
-void error_locator8(const uint32_t* erased, uint32_t* el_bytes) {
-    thread_local uint32_t last_pattern[8] = {~0u, 0, 0, 0, 0, 0, 0, 0};
-    thread_local uint32_t last_el[kFf8Ptrs / 4];
-    if (std::memcmp(last_pattern, erased, sizeof(last_pattern)) != 0) {
-        const GaloisField& f = field8();
-        uint16_t e[256];
-        for (unsigned p = 0; p < 256; ++p) e[p] = (erased[p >> 5] >> (p & 31)) & 1u;
-        f.walsh(e, 256);
-        for (unsigned p = 0; p < 256; ++p) e[p] = uint16_t((unsigned(e[p]) * f.log_walsh[p]) % 255u);
-        f.walsh(e, 256);
-        for (unsigned q = 0; q < 64; ++q)
-            last_el[q] = uint32_t(e[4 * q] % 255u) | uint32_t(e[4 * q + 1] % 255u) << 8 |
-                         uint32_t(e[4 * q + 2] % 255u) << 16 | uint32_t(e[4 * q + 3] % 255u) << 24;
-        std::memcpy(last_pattern, erased, sizeof(last_pattern));
-    }
-    std::memcpy(el_bytes, last_el, sizeof(last_el));
-}
-
 // LEO_AMD_FF8_HALF=0 turns the half-position decoders (FF8 kernel, FF16 pass 2)
 // off (A/B experiments); read once.
 bool ff8_half_decoder_enabled() {
-    static const bool v = [] {
-        const char* e = std::getenv("LEO_AMD_FF8_HALF");
-        return !(e && e[0] == '0');
-    }();
+    static const bool v = !experiment_off("LEO_AMD_FF8_HALF");
     return v;
 }
 
 // LEO_AMD_FF8_SPLIT=0 turns the split partial-loss decoder off (A/B); read once.
 bool ff8_split_decoder_enabled() {
-    static const bool v = [] {
-        const char* e = std::getenv("LEO_AMD_FF8_SPLIT");
-        return !(e && e[0] == '0');
-    }();
+    static const bool v = !experiment_off("LEO_AMD_FF8_SPLIT");
     return v;
 }
 
@@ -561,7 +681,8 @@ int fill_dec8(Ff8DecArgs& a, const DeviceTables* t, unsigned K, unsigned R, cons
     }
     std::memcpy(a.present, pc.present, sizeof(a.present));
     std::memcpy(a.needed, pc.needed, sizeof(a.needed));
-    error_locator8(erased, a.el);
+    std::memcpy(a.erased, erased, sizeof(a.erased));  // the kernels compute the error locator from it
+    a.walsh = t->walsh8;
     a.sktab = t->sktab8;
     a.tabs = t->tab8;
     a.K = K;
@@ -584,10 +705,7 @@ int fill_dec8(Ff8DecArgs& a, const DeviceTables* t, unsigned K, unsigned R, cons
 
 // LEO_AMD_FF8_INVERT=0 turns the inverse full-loss decoder off (A/B); read once.
 bool ff8_invert_enabled() {
-    static const bool v = [] {
-        const char* e = std::getenv("LEO_AMD_FF8_INVERT");
-        return !(e && e[0] == '0');
-    }();
+    static const bool v = !experiment_off("LEO_AMD_FF8_INVERT");
     return v;
 }
 
@@ -681,7 +799,8 @@ LeopardResult decode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
     const size_t off_rl = off_sl + 65536 * 4;
     const size_t dec16_bytes = off_rl + 65536 * 4;
     Workspace& ws = *c.ws;
-    if (!ws.dec16) HIP_OK(hipMalloc(reinterpret_cast<void**>(&ws.dec16), dec16_bytes), "allocate decoder state");
+    ws.touched = true;
+    if (!ws.dec16) HIP_OK(hipMallocAsync(reinterpret_cast<void**>(&ws.dec16), dec16_bytes, c.s), "allocate decoder state");
     std::vector<uint32_t> key(2 + bitmap_words, 0);
     key[0] = K;
     key[1] = R;
@@ -873,11 +992,15 @@ uint64_t pipe_slot_budget() {
 //   2  the kernels read the inputs from and write the outputs to the pinned slot
 //      over PCIe (no SDMA copies at all).
 int pipe_mode() {
+#if LAMD_EXPERIMENT_ENV
     static const int v = [] {
         const char* e = std::getenv("LEO_AMD_PIPE_MODE");
         return e && e[0] >= '0' && e[0] <= '2' ? e[0] - '0' : kDefaultPipeMode;
     }();
     return v;
+#else
+    return kDefaultPipeMode;
+#endif
 }
 
 // hin: host input pieces (call offset applied); hout: host output pieces.
@@ -927,6 +1050,7 @@ LeopardResult run_host_pipeline(Call& c, uint64_t bytes, const std::vector<const
                         : fn(cs, len, mapped, mapped + in_bytes, slice);
         if (r != Leopard_Success) return r;
         HIP_OK(hipGetLastError(), "kernel launch");
+        if ((r = cs.ws->mark_use(cs.s)) != Leopard_Success) return r;
         if (mode == 0)
             HIP_OK(hipMemcpyAsync(pin + in_bytes, dev + in_bytes, nout * slice, hipMemcpyDeviceToHost, cs.s),
                    "slice download");
@@ -1080,18 +1204,21 @@ int pick_device(const void* first, MemKind* kind) {
     return cur;
 }
 
-struct DeviceGuard {
-    int prev = -1;
-    explicit DeviceGuard(int dev) {
-        (void)hipGetDevice(&prev);
-        if (prev != dev) (void)hipSetDevice(dev);
-    }
-    ~DeviceGuard() {
-        int cur = -1;
-        (void)hipGetDevice(&cur);
-        if (prev >= 0 && cur != prev) (void)hipSetDevice(prev);
-    }
-};
+// A NULL destination for a piece the call must write (recovery piece j < R on
+// encode, the work piece of a lost original on decode).  The reference would
+// write through it (leopard.cpp:123-344 validates only the arrays); here it is
+// Leopard_InvalidInput, decided where the work is done: per column range on
+// the fan-out workers, whose failure then reaches the caller.
+LeopardResult missing_output(void* const* outs, unsigned count, const void* const* lost_if) {
+    for (unsigned i = 0; i < count; ++i)
+        if (!outs[i] && (!lost_if || !lost_if[i])) {
+            char buf[96];
+            std::snprintf(buf, sizeof(buf), "work_data[%u] is NULL but the call writes it", i);
+            tls.last_error = buf;
+            return Leopard_InvalidInput;
+        }
+    return Leopard_Success;
+}
 
 LeopardResult encode_any(uint64_t bytes, uint64_t off, unsigned K, unsigned R, const void* const* orig, void** work) {
     MemKind kind;
@@ -1102,6 +1229,7 @@ LeopardResult encode_any(uint64_t bytes, uint64_t off, unsigned K, unsigned R, c
     if (r != Leopard_Success) return r;
 
     if (kind == MemKind::Device) {
+        if ((r = missing_output(work, R, nullptr)) != Leopard_Success) return r;
         if (K == 1) {  // leopard.cpp:144-149
             for (unsigned i = 0; i < R; ++i)
                 HIP_OK(hipMemcpyAsync(static_cast<uint8_t*>(work[i]) + off, static_cast<const uint8_t*>(orig[i]) + off,
@@ -1118,6 +1246,7 @@ LeopardResult encode_any(uint64_t bytes, uint64_t off, unsigned K, unsigned R, c
 
     // host memory (leopard.cpp:143-149: K == 1 is a copy)
     if (K == 1) {
+        if ((r = missing_output(work, R, nullptr)) != Leopard_Success) return r;
         std::vector<CopyJob> jobs;
         for (unsigned i = 0; i < R; ++i)
             jobs.push_back({static_cast<uint8_t*>(work[i]) + off, static_cast<const uint8_t*>(orig[i]) + off, bytes});
@@ -1129,6 +1258,7 @@ LeopardResult encode_any(uint64_t bytes, uint64_t off, unsigned K, unsigned R, c
         if (nr > 1)
             return fanout(nr, bytes, [&](uint64_t len, uint64_t o) { return encode_any(len, off + o, K, R, orig, work); });
     }
+    if ((r = missing_output(work, R, nullptr)) != Leopard_Success) return r;
     // Device work of one column slice staged as dense rows: inputs = the K
     // originals, outputs = the R recovery pieces.
     const SliceFn slice_fn = [&](Call& cs, uint64_t len, uint8_t* din, uint8_t* dout, uint64_t stride) {
@@ -1182,6 +1312,8 @@ LeopardResult decode_any(uint64_t bytes, uint64_t off, unsigned K, unsigned R, c
     const void* k1_src = K == 1 ? (rec[got_i] ? rec[got_i] : orig[0]) : nullptr;
 
     if (kind == MemKind::Device) {
+        if ((r = missing_output(work, K == 1 ? 1 : K, K == 1 || lost == 0 ? nullptr : orig)) != Leopard_Success)
+            return r;
         if (K == 1) {  // leopard.cpp:279-283
             HIP_OK(hipMemcpyAsync(static_cast<uint8_t*>(work[0]) + off, static_cast<const uint8_t*>(k1_src) + off,
                                   bytes, hipMemcpyDeviceToDevice, c.s),
@@ -1206,6 +1338,7 @@ LeopardResult decode_any(uint64_t bytes, uint64_t off, unsigned K, unsigned R, c
 
     // host memory: K == 1 and zero loss are copies (leopard.cpp:279-291)
     if (K == 1 || lost == 0) {
+        if ((r = missing_output(work, K == 1 ? 1 : K, nullptr)) != Leopard_Success) return r;
         std::vector<CopyJob> jobs;
         if (K == 1) jobs.push_back({static_cast<uint8_t*>(work[0]) + off, static_cast<const uint8_t*>(k1_src) + off, bytes});
         else
@@ -1220,6 +1353,7 @@ LeopardResult decode_any(uint64_t bytes, uint64_t off, unsigned K, unsigned R, c
             return fanout(nr, bytes,
                           [&](uint64_t len, uint64_t o) { return decode_any(len, off + o, K, R, orig, rec, work); });
     }
+    if ((r = missing_output(work, K, orig)) != Leopard_Success) return r;
     // Device work of one column slice staged as dense rows: inputs = received
     // recoveries, then received originals (so the R == 1 XOR sources form one
     // slab); outputs = lost originals in order.
@@ -1330,16 +1464,43 @@ LeopardResult decode_checked(uint64_t bytes, uint64_t off, unsigned K, unsigned 
 // object's column strips (argument blocks uploaded through the staging ring),
 // so a batch of small objects fills the GPU where a single 64 KiB-piece call
 // gives each CU one workgroup; anything else runs object by object.
-bool batch_on_device(unsigned count, const void* const* firsts, int* dev) {
-    MemKind kind;
-    *dev = pick_device(firsts[0], &kind);
-    if (kind != MemKind::Device) return false;
-    for (unsigned o = 1; o < count; ++o) {
+//
+// The one-launch path is taken only when every piece the kernel touches (every
+// input read and every output written, of every object) lies in device memory
+// of that one device.  Pieces are checked against the allocation ranges
+// already seen (hipMemGetAddressRange), so a slab-laid object costs two range
+// checks and a batch a handful of runtime queries.
+struct RangeCache {
+    struct Range {
+        uintptr_t lo, hi;
+        int dev;
+    };
+    std::vector<Range> seen;
+    // [p, p + len) inside one device allocation of device dev
+    bool on(const void* p, uint64_t len, int dev) {
+        if (!p) return false;
+        const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+        for (const Range& x : seen)
+            if (a >= x.lo && a < x.hi) return x.dev == dev && a + len <= x.hi;
         int d = -1;
-        if (classify(firsts[o], &d) != MemKind::Device || d != *dev) return false;
+        if (classify(p, &d) != MemKind::Device) return false;
+        void* base = nullptr;
+        size_t size = 0;
+        if (hipMemGetAddressRange(&base, &size, const_cast<void*>(p)) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        const uintptr_t lo = reinterpret_cast<uintptr_t>(base);
+        seen.push_back({lo, lo + size, d});
+        return d == dev && a + len <= lo + size;
     }
-    return true;
-}
+    // every non-null piece of p[0, n)
+    bool all_on(const void* const* p, unsigned n, uint64_t len, int dev) {
+        for (unsigned i = 0; i < n; ++i)
+            if (p[i] && !on(p[i], len, dev)) return false;
+        return true;
+    }
+};
 
 // Pieces p[0, n) equally spaced (a slab) with a stride that fits a signed
 // 32-bit integer (Ff8SlabBatch): base and stride (two's complement).
@@ -1352,19 +1513,27 @@ bool slab_of(const void* const* p, unsigned n, uint64_t& base, int32_t& stride) 
         if (!p[i] || uint64_t(reinterpret_cast<uintptr_t>(p[i])) != base + uint64_t(int64_t(i) * s)) return false;
     return true;
 }
+// the bytes a slab of n pieces of `len` bytes spans, inside one allocation of dev
+bool slab_on(RangeCache& rc, uint64_t base, int32_t stride, unsigned n, uint64_t len, int dev) {
+    const int64_t span = int64_t(n - 1) * stride;
+    const uint64_t lo = base + uint64_t(std::min<int64_t>(0, span));
+    const uint64_t hi = base + uint64_t(std::max<int64_t>(0, span)) + len;
+    return rc.on(reinterpret_cast<const void*>(uintptr_t(lo)), hi - lo, dev);
+}
 
-// Batch of objects whose `nin` inputs and `nout` outputs are slabs: launches
-// of up to kSlabObjs objects with every argument by value (no upload in front
-// of the kernel).  Returns false (nothing launched) when some object is not
-// slab-laid.
-bool run_slab_batch8(int dev, unsigned count, uint64_t bytes, unsigned T, unsigned K, unsigned R, unsigned nin,
-                     unsigned nout, const void* const* const* ins, void* const* const* outs, bool multi, int form,
-                     LeopardResult* res) {
+// Batch of objects whose `nin` inputs and `nout` outputs are slabs on device
+// dev: launches of up to kSlabObjs objects with every argument by value (no
+// upload in front of the kernel).  Returns false (nothing launched) when some
+// object is not slab-laid there.
+bool run_slab_batch8(int dev, RangeCache& rc, unsigned count, uint64_t bytes, unsigned T, unsigned K, unsigned R,
+                     unsigned nin, unsigned nout, const void* const* const* ins, void* const* const* outs, bool multi,
+                     int form, LeopardResult* res) {
     std::vector<uint64_t> ib(count), ob(count);
     std::vector<int32_t> is(count), os(count);
     for (unsigned o = 0; o < count; ++o)
         if (!slab_of(ins[o], nin, ib[o], is[o]) ||
-            !slab_of(const_cast<const void* const*>(outs[o]), nout, ob[o], os[o]))
+            !slab_of(const_cast<const void* const*>(outs[o]), nout, ob[o], os[o]) ||
+            !slab_on(rc, ib[o], is[o], nin, bytes, dev) || !slab_on(rc, ob[o], os[o], nout, bytes, dev))
             return false;
     *res = [&]() -> LeopardResult {
         DeviceGuard guard(dev);
@@ -1424,25 +1593,28 @@ LeopardResult encode_batch(unsigned count, uint64_t bytes, unsigned K, unsigned 
     }
     if (count == 0) return Leopard_Success;
     const unsigned m = next_pow2(R), n = next_pow2(m + K);
-    std::vector<const void*> firsts(count);
-    for (unsigned o = 0; o < count; ++o) firsts[o] = orig[o][0];
-    int dev = -1;
-    if (K > 1 && R > 1 && n <= 256 && bytes <= kFf8MaxLaunchBytes && batch_on_device(count, firsts.data(), &dev)) {
+    MemKind kind = MemKind::Host;
+    const int dev = K > 1 && R > 1 && n <= 256 && bytes <= kFf8MaxLaunchBytes ? pick_device(orig[0][0], &kind) : -1;
+    if (kind == MemKind::Device) {
         const unsigned Tm = log2u(m);
         const bool multi = (K + m - 1) / m > 1;
         const int form = K == m && R == m ? kFormDenseEnc : kFormGeneral;
+        RangeCache rc;
         LeopardResult res;
-        if (run_slab_batch8(dev, count, bytes, Tm, K, R, K, R, orig, work, multi, form, &res)) return res;
-        return run_batch8<Ff8EncArgs>(
-            dev, count,
-            [&](Ff8EncArgs& a, const DeviceTables* t, unsigned o) {
-                fill_enc8(a, t, K, R, orig[o], work[o], 0, bytes);
-                return 0;
-            },
-            [&](const Ff8EncArgs* d, int, hipStream_t s) {
-                return launch_ff8_encode_batch(Tm, d, count, uint32_t(bytes / 4), (K + m - 1) / m > 1,
-                                               K == m && R == m ? kFormDenseEnc : kFormGeneral, s);
-            });
+        if (run_slab_batch8(dev, rc, count, bytes, Tm, K, R, K, R, orig, work, multi, form, &res)) return res;
+        bool on_dev = true;
+        for (unsigned o = 0; o < count && on_dev; ++o)
+            on_dev = rc.all_on(orig[o], K, bytes, dev) && rc.all_on(const_cast<const void* const*>(work[o]), R, bytes, dev);
+        if (on_dev)
+            return run_batch8<Ff8EncArgs>(
+                dev, count,
+                [&](Ff8EncArgs& a, const DeviceTables* t, unsigned o) {
+                    fill_enc8(a, t, K, R, orig[o], work[o], 0, bytes);
+                    return 0;
+                },
+                [&](const Ff8EncArgs* d, int, hipStream_t s) {
+                    return launch_ff8_encode_batch(Tm, d, count, uint32_t(bytes / 4), multi, form, s);
+                });
     }
     for (unsigned o = 0; o < count; ++o) {
         const LeopardResult r = encode_any(bytes, 0, K, R, orig[o], work[o]);
@@ -1472,31 +1644,40 @@ LeopardResult decode_batch(unsigned count, uint64_t bytes, unsigned K, unsigned 
     }
     if (count == 0) return Leopard_Success;
     const unsigned m = next_pow2(R), n = next_pow2(m + K);
+    MemKind kind = MemKind::Host;
     int dev = -1;
     if (general && n <= 256 && bytes <= kFf8MaxLaunchBytes) {
-        std::vector<const void*> firsts(count);
-        for (unsigned o = 0; o < count; ++o) {
-            const void* f = nullptr;
-            for (unsigned i = 0; i < R && !f; ++i) f = rec[o][i];
-            firsts[o] = f;
+        const void* first = nullptr;  // the device rule of decode_any
+        for (unsigned i = 0; i < K && !first; ++i) first = orig[0][i];
+        for (unsigned i = 0; i < R && !first; ++i) first = rec[0][i];
+        dev = pick_device(first, &kind);
+    }
+    if (kind == MemKind::Device) {
+        const unsigned Tn = log2u(n);
+        bool full = true;  // every object a full loss of a K = R = m code: the inverse encoder tile
+        for (unsigned o = 0; o < count && full; ++o) full = full_loss_square(K, R, orig[o], rec[o]);
+        RangeCache rc;
+        LeopardResult res;
+        if (full && run_slab_batch8(dev, rc, count, bytes, Tn - 1, m, m, m, m, rec, work, false, kFormDenseDec, &res))
+            return res;
+        // inputs: received originals and recoveries; outputs: the work pieces of lost originals
+        bool on_dev = true;
+        for (unsigned o = 0; o < count && on_dev; ++o) {
+            on_dev = rc.all_on(orig[o], K, bytes, dev) && rc.all_on(rec[o], R, bytes, dev);
+            for (unsigned i = 0; i < K && on_dev; ++i)
+                if (!orig[o][i]) on_dev = rc.on(work[o][i], bytes, dev);
         }
-        if (batch_on_device(count, firsts.data(), &dev)) {
-            const unsigned Tn = log2u(n);
-            bool full = true;  // every object a full loss of a K = R = m code: the inverse encoder tile
-            for (unsigned o = 0; o < count && full; ++o) full = full_loss_square(K, R, orig[o], rec[o]);
-            LeopardResult res;
-            if (full && run_slab_batch8(dev, count, bytes, Tn - 1, m, m, m, m, rec, work, false, kFormDenseDec, &res))
-                return res;
-            if (full)
-                return run_batch8<Ff8EncArgs>(
-                    dev, count,
-                    [&](Ff8EncArgs& a, const DeviceTables* t, unsigned o) {
-                        fill_dec8_full(a, t, m, rec[o], work[o], 0, bytes);
-                        return 0;
-                    },
-                    [&](const Ff8EncArgs* d, int, hipStream_t s) {
-                        return launch_ff8_encode_batch(Tn - 1, d, count, uint32_t(bytes / 4), false, kFormDenseDec, s);
-                    });
+        if (on_dev && full)
+            return run_batch8<Ff8EncArgs>(
+                dev, count,
+                [&](Ff8EncArgs& a, const DeviceTables* t, unsigned o) {
+                    fill_dec8_full(a, t, m, rec[o], work[o], 0, bytes);
+                    return 0;
+                },
+                [&](const Ff8EncArgs* d, int, hipStream_t s) {
+                    return launch_ff8_encode_batch(Tn - 1, d, count, uint32_t(bytes / 4), false, kFormDenseDec, s);
+                });
+        if (on_dev)
             return run_batch8<Ff8DecArgs>(
                 dev, count,
                 [&](Ff8DecArgs& a, const DeviceTables* t, unsigned o) {
@@ -1506,7 +1687,6 @@ LeopardResult decode_batch(unsigned count, uint64_t bytes, unsigned K, unsigned 
                     return launch_ff8_decode_batch(mode != kDec8General ? Tn - 1 : Tn, d, count, uint32_t(bytes / 4),
                                                    mode, s);
                 });
-        }
     }
     for (unsigned o = 0; o < count; ++o) {
         const LeopardResult r = decode_any(bytes, 0, K, R, orig[o], rec[o], work[o]);
@@ -1553,6 +1733,7 @@ LEO_EXPORT int leo_init_(int version) {
     g_dev.assign(count, DeviceTables{});
     g_device_count = count;
     g_initialized = true;
+    std::atexit([] { g_exiting.store(true); });  // after the runtime's own registration: runs before its teardown
     return Leopard_Success;
 }
 
@@ -1674,6 +1855,9 @@ LEO_EXPORT void leo_amd_set_stream(void* hip_stream) { tls.stream = static_cast<
 LEO_EXPORT void leo_amd_set_async(int async_enable) { tls.async = async_enable != 0; }
 LEO_EXPORT void leo_amd_set_device(int device) { tls.device = device; }
 LEO_EXPORT void leo_amd_set_fanout(int ranges) { tls.fanout = ranges; }
+LEO_EXPORT void leo_amd_release_stream(void* hip_stream) {
+    release_workspaces(static_cast<hipStream_t>(hip_stream), hip_stream == reinterpret_cast<void*>(intptr_t(-1)));
+}
 
 LEO_EXPORT int leo_amd_device_count(void) {
     int count = 0;

@@ -98,7 +98,8 @@ struct Ff8DecArgs {
     uint64_t ptr[kFf8Ptrs];        // position p: received piece / output of a lost original / 0
     uint32_t present[kPyr8Words];  // pyramid of received positions (Pyr8Live)
     uint32_t needed[kPyr8Words];   // pyramid of lost originals
-    uint32_t el[kFf8Ptrs / 4];     // error locator logs (host computed), one byte per position
+    uint32_t erased[kFf8Ptrs / 32]; // erasure bitmap over the 256 positions (LeopardFF8.cpp:1825-1840)
+    const uint32_t* walsh;         // LogWalsh (256 entries): the kernels compute the error locator
     const uint32_t* sktab;
     const uint32_t* tabs;          // multiply tables by log value; entry 256 is all zero
     const uint32_t* fused;         // k_ff8_dec_half: fused top-layer table of this m (= encoder chunk 0's)
@@ -111,6 +112,8 @@ struct Ff8DecArgs {
 // (ordered from the least specialised: a batch runs the minimum over its objects;
 // the split decoder also handles the half kinds, with no high-half input)
 constexpr int kDec8General = 0, kDec8Split = 1, kDec8Half = 2, kDec8HalfDense = 3;
+// LDS dwords of the in-kernel GF(2^8) error locator (one byte per position)
+constexpr size_t kEl8Dwords = kFf8Ptrs / 4;
 // Forms of the GF(2^8) encoder tile (k_ff8_enc): general (pruned, chunked),
 // dense encode (one chunk, K = R = m), dense inverse (full-loss decode of a
 // K = R = m code, launch_ff8_decode_full).

@@ -34,6 +34,12 @@
 #ifndef LAMD_ABLATE
 #define LAMD_ABLATE 0
 #endif
+// 1: the library reads the A/B experiment switches (LEO_AMD_FF8_WIDE,
+// LEO_AMD_FF8_HALF / SPLIT / INVERT, LEO_AMD_PIPE_MODE) from the environment;
+// tools/ builds only.  The shipped library always takes the tested defaults.
+#ifndef LAMD_EXPERIMENT_ENV
+#define LAMD_EXPERIMENT_ENV 0
+#endif
 #ifndef LAMD_FF16_PREFETCH
 #define LAMD_FF16_PREFETCH 0
 #endif

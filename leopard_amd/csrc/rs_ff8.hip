@@ -380,7 +380,51 @@ __global__ void __launch_bounds__(threads_for(T, RB), LAMD_SLAB_WAVES) k_ff8_enc
 
 // --------------------------------------------------------------- decode -----
 
-LDEV unsigned el_at(const Ff8DecArgs& a, unsigned p) { return (a.el[p >> 2] >> ((p & 3) * 8)) & 0xFFu; }
+// Error locator of the decoders (LeopardFF8.cpp:1845-1853, FWHT :80-130):
+//   el = FWHT( LogWalsh * FWHT(erasures) )  mod 255,
+// a 256-point Walsh-Hadamard transform mod 255, twice.  Wave 0 of every
+// workgroup computes it in the prologue, while the other waves wait for their
+// piece loads: 4 positions a lane (p = lane + 64 j), six layers across lanes
+// (__shfl_xor) and two in registers.  Fully reduced mod 255 (the reference
+// reduces partially, 255 standing for 0: the same residues; the multiply tables
+// of log 0 and log 255 are the same, x * exp(0) = x * exp(255)).  The result
+// lands in LDS, one byte per position.
+struct Mod8 {
+    LDEV static unsigned add(unsigned a, unsigned b) { const unsigned s = a + b; return s >= 255u ? s - 255u : s; }
+    LDEV static unsigned sub(unsigned a, unsigned b) { const unsigned s = a + 255u - b; return s >= 255u ? s - 255u : s; }
+};
+LDEV void fwht256_mod255(unsigned (&e)[4], unsigned lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const unsigned o = unsigned(__shfl_xor(int(e[j]), d));
+            e[j] = (lane & d) ? Mod8::sub(o, e[j]) : Mod8::add(e[j], o);
+        }
+    const unsigned a0 = Mod8::add(e[0], e[1]), a1 = Mod8::sub(e[0], e[1]);
+    const unsigned a2 = Mod8::add(e[2], e[3]), a3 = Mod8::sub(e[2], e[3]);
+    e[0] = Mod8::add(a0, a2);
+    e[2] = Mod8::sub(a0, a2);
+    e[1] = Mod8::add(a1, a3);
+    e[3] = Mod8::sub(a1, a3);
+}
+LDEV void error_locator8(const Ff8DecArgs& a, uint8_t* el, unsigned wave, unsigned lane) {
+    if (wave != 0) return;
+    unsigned e[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const unsigned p = lane + 64u * j;
+        e[j] = (cload(a.erased + (p >> 5)) >> (p & 31)) & 1u;
+    }
+    if constexpr ((LAMD_ABLATE & 32) == 0) {
+        fwht256_mod255(e, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) e[j] = (e[j] * a.walsh[lane + 64u * j]) % 255u;
+        fwht256_mod255(e, lane);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) el[lane + 64u * j] = uint8_t(e[j]);
+}
 
 // v[r] *= table(log_of(r)) for the pieces with pred(r): the tables of KB pieces
 // are read together, then their multiplies run (one LDS round trip per batch).
@@ -407,6 +451,7 @@ LDEV void ff8_dec(const Ff8DecArgs& a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const LdsTab8<256> sk{lds + areas8(NA) * tile_dwords_for(T, RB)};
     const LdsTab8<256> ltab{sk.base + LdsTab8<256>::kDwords};  // by log value
+    uint8_t* el = reinterpret_cast<uint8_t*>(ltab.base + LdsTab8<256>::kDwords);
     LdsRing<tile_dwords_for(T, RB), areas8(NA)> ring{lds};
     STAMP(0);
     TabStage8<threads_for(T, RB), 256> sk_stage, log_stage;
@@ -417,6 +462,7 @@ LDEV void ff8_dec(const Ff8DecArgs& a) {
     const PieceSpace ps{0, 0, 0};
     const Pyr8Live present{a.present}, needed{a.needed};
     auto pos = [&](int r) { return TL::piece(0, r, w); };
+    auto el_at = [&](unsigned p) { return unsigned(el[p]); };
     typename TL::Reg v;
     {
         // received pieces: positions [0, R) recovery, [m, m + K) originals (LeopardFF8.cpp:1857-1877)
@@ -426,12 +472,13 @@ LDEV void ff8_dec(const Ff8DecArgs& a) {
         for (int r = 0; r < TL::NR; ++r) v[r][0] = present(pos(r), 0) ? gload(pp[r], cl) : 0u;
     }
     STAMP(1);
+    error_locator8(a, el, w, lane);
     sk_stage.store(sk);
     log_stage.store(ltab);
     __syncthreads();
     STAMP(2);
     // scale by exp(el) (absent pieces stay zero)
-    scale_batched<TL>(v, ltab, [&](int r) { return el_at(a, pos(r)); }, [&](int r) { return present(pos(r), 0); });
+    scale_batched<TL>(v, ltab, [&](int r) { return el_at(pos(r)); }, [&](int r) { return present(pos(r), 0); });
     Skew8Win win{{sk}};
     win.stage(nullptr, -1);
     // IFFT and FFT without their top layers around swap_top + D_low (see
@@ -455,7 +502,7 @@ LDEV void ff8_dec(const Ff8DecArgs& a) {
     uint64_t pp[TL::NR];
     fetch_ptrs(pp, a, pos);
     auto is_needed = [&](int r) { return needed(pos(r), 0); };
-    scale_batched<TL>(v, ltab, [&](int r) { return F::kModulus - el_at(a, pos(r)); }, is_needed);
+    scale_batched<TL>(v, ltab, [&](int r) { return F::kModulus - el_at(pos(r)); }, is_needed);
     if (!cl.live) return;
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r)
@@ -494,6 +541,8 @@ LDEV void ff8_dec_half(const Ff8DecArgs& a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const LdsTab8<256> sk{lds + tile_dwords_for(T, RB)};
     const LdsTab8<256> ltab{sk.base + LdsTab8<256>::kDwords};  // by log value
+    uint8_t* el = reinterpret_cast<uint8_t*>(ltab.base + LdsTab8<256>::kDwords);
+    auto el_at = [&](unsigned p) { return unsigned(el[p]); };
     TabStage8<threads_for(T, RB), 256> sk_stage, log_stage;
     sk_stage.load(a.sktab);
     log_stage.load(a.tabs);
@@ -514,10 +563,11 @@ LDEV void ff8_dec_half(const Ff8DecArgs& a) {
 #pragma unroll
         for (int r = 0; r < TL::NR; ++r) v[r][0] = present(lpos(r), 0) ? gload(pp[r], cl) : 0u;
     }
+    error_locator8(a, el, w, lane);
     sk_stage.store(sk);
     log_stage.store(ltab);
     __syncthreads();
-    scale_batched<TL>(v, ltab, [&](int r) { return el_at(a, lpos(r)); }, [&](int r) { return present(lpos(r), 0); });
+    scale_batched<TL>(v, ltab, [&](int r) { return el_at(lpos(r)); }, [&](int r) { return present(lpos(r), 0); });
     Skew8Win win{{sk}};
     win.stage(nullptr, -1);  // decoder skew base (LeopardFF8.cpp:1880, 1903)
     // both top layers (single skews m/2 - 1 and m + m/2 - 1) as one butterfly
@@ -529,7 +579,7 @@ LDEV void ff8_dec_half(const Ff8DecArgs& a) {
     uint64_t pp[TL::NR];
     fetch_ptrs(pp, a, hpos);
     auto is_needed = [&](int r) { return needed(hpos(r), 0); };
-    scale_batched<TL>(v, ltab, [&](int r) { return F::kModulus - el_at(a, hpos(r)); }, is_needed);
+    scale_batched<TL>(v, ltab, [&](int r) { return F::kModulus - el_at(hpos(r)); }, is_needed);
     if (!cl.live) return;
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r)
@@ -565,6 +615,8 @@ LDEV void ff8_dec_split(const Ff8DecArgs& a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const LdsTab8<256> sk{lds + tile_dwords_for(T, RB)};
     const LdsTab8<256> ltab{sk.base + LdsTab8<256>::kDwords};  // by log value
+    uint8_t* el = reinterpret_cast<uint8_t*>(ltab.base + LdsTab8<256>::kDwords);
+    auto el_at = [&](unsigned p) { return unsigned(el[p]); };
     TabStage8<threads_for(T, RB), 256> sk_stage, log_stage;
     sk_stage.load(a.sktab);
     log_stage.load(a.tabs);
@@ -584,19 +636,20 @@ LDEV void ff8_dec_split(const Ff8DecArgs& a) {
 #pragma unroll
         for (int r = 0; r < TL::NR; ++r) x[r][0] = present(lpos(r), 0) ? gload(pp[r], cl) : 0u;
     }
+    error_locator8(a, el, w, lane);
     sk_stage.store(sk);
     log_stage.store(ltab);
     __syncthreads();
     Skew8Win win{{sk}};
     win.stage(nullptr, -1);  // decoder skew base (LeopardFF8.cpp:1880, 1903)
     // y = N(I_H(h * exp(el)))
-    scale_batched<TL>(h, ltab, [&](int r) { return el_at(a, hpos(r)); }, [&](int r) { return present(hpos(r), 0); });
+    scale_batched<TL>(h, ltab, [&](int r) { return el_at(hpos(r)); }, [&](int r) { return present(hpos(r), 0); });
     TL::template ifft<false>(h, w, lane, lds, high, win, present);
     typename TL::Reg y;
     TL::zero(y);
     TL::derivative_add(y, [&](int r, uint32_t* out) { out[0] = h[r][0]; }, w, lane, lds);
     // x <- I_L(x * exp(el)) ^ y, then F_H
-    scale_batched<TL>(x, ltab, [&](int r) { return el_at(a, lpos(r)); }, [&](int r) { return present(lpos(r), 0); });
+    scale_batched<TL>(x, ltab, [&](int r) { return el_at(lpos(r)); }, [&](int r) { return present(lpos(r), 0); });
     TL::template ifft<false>(x, w, lane, lds, low, win, present);
     TL::xor_into(x, y);
     TL::template fft<false>(x, w, lane, lds, high, win, needed);
@@ -604,7 +657,7 @@ LDEV void ff8_dec_split(const Ff8DecArgs& a) {
     uint64_t pp[TL::NR];
     fetch_ptrs(pp, a, hpos);
     auto is_needed = [&](int r) { return needed(hpos(r), 0); };
-    scale_batched<TL>(x, ltab, [&](int r) { return F::kModulus - el_at(a, hpos(r)); }, is_needed);
+    scale_batched<TL>(x, ltab, [&](int r) { return F::kModulus - el_at(hpos(r)); }, is_needed);
     if (!cl.live) return;
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r)
@@ -676,11 +729,15 @@ struct DecSplitTag {};
 // Launch shape overrides for experiments (LEO_AMD_FF8_WIDE=1: the wide
 // register forms at every size); read once.
 bool force_wide() {
+#if LAMD_EXPERIMENT_ENV
     static const bool v = [] {
         const char* e = std::getenv("LEO_AMD_FF8_WIDE");
         return e && e[0] == '1';
     }();
     return v;
+#else
+    return false;  // experiment builds only (LAMD_EXPERIMENT_ENV=1)
+#endif
 }
 
 // Lane-group bits of the encoder launch (LEO_AMD_FF8_G overrides; read once):
@@ -732,7 +789,7 @@ hipError_t enc_T(const Ff8EncArgs& a, hipStream_t s) {
 }
 template <int T, int RB, int NA>
 hipError_t dec_RB(const Ff8DecArgs& a, hipStream_t s) {
-    constexpr size_t lds = areas8(NA) * tile_dwords_for(T, RB) + 2 * LdsTab8<256>::kDwords;
+    constexpr size_t lds = areas8(NA) * tile_dwords_for(T, RB) + 2 * LdsTab8<256>::kDwords + kEl8Dwords;
     return launch8<DecTag<T, RB, NA>>(&k_ff8_dec<T, RB, NA>, threads_for(T, RB), a, lds, s);
 }
 template <int T>
@@ -747,7 +804,7 @@ hipError_t dec_T(const Ff8DecArgs& a, hipStream_t s) {
 template <int T>
 hipError_t dec_half_T(const Ff8DecArgs& a, hipStream_t s) {
     constexpr int RB = reg_bits8(T);
-    constexpr size_t lds = tile_dwords_for(T, RB) + 2 * LdsTab8<256>::kDwords;
+    constexpr size_t lds = tile_dwords_for(T, RB) + 2 * LdsTab8<256>::kDwords + kEl8Dwords;
     if (a.dense)
         return launch8<DecHalfTag<T, RB + 16>>(&k_ff8_dec_half<T, RB, true>, threads_for(T, RB), a, lds, s);
     return launch8<DecHalfTag<T, RB>>(&k_ff8_dec_half<T, RB, false>, threads_for(T, RB), a, lds, s);
@@ -755,7 +812,7 @@ hipError_t dec_half_T(const Ff8DecArgs& a, hipStream_t s) {
 template <int T>
 hipError_t dec_split_T(const Ff8DecArgs& a, hipStream_t s) {
     constexpr int RB = reg_bits8(T);
-    constexpr size_t lds = tile_dwords_for(T, RB) + 2 * LdsTab8<256>::kDwords;
+    constexpr size_t lds = tile_dwords_for(T, RB) + 2 * LdsTab8<256>::kDwords + kEl8Dwords;
     return launch8<DecSplitTag<T, RB>>(&k_ff8_dec_split<T, RB>, threads_for(T, RB), a, lds, s);
 }
 
@@ -869,7 +926,7 @@ hipError_t launch_ff8_decode_batch(unsigned T, const Ff8DecArgs* objs, unsigned 
     if (mode != kDec8General) {
         static_for<1, 8>([&](auto I) {
             constexpr int TT = decltype(I)::value, RB = batch_bits8(TT);
-            constexpr size_t lds = tile_dwords_for(TT, RB) + 2 * LdsTab8<256>::kDwords;
+            constexpr size_t lds = tile_dwords_for(TT, RB) + 2 * LdsTab8<256>::kDwords + kEl8Dwords;
             if (T != unsigned(TT)) return;
             if (mode == kDec8Split)
                 e = launch8_batch<DecSplitBatchTag<TT>>(&k_ff8_dec_split_batch<TT, RB>, threads_for(TT, RB), objs,
@@ -885,7 +942,7 @@ hipError_t launch_ff8_decode_batch(unsigned T, const Ff8DecArgs* objs, unsigned 
     }
     static_for<1, 9>([&](auto I) {
         constexpr int TT = decltype(I)::value, RB = batch_bits8(TT);
-        constexpr size_t lds = tile_dwords_for(TT, RB) + 2 * LdsTab8<256>::kDwords;
+        constexpr size_t lds = tile_dwords_for(TT, RB) + 2 * LdsTab8<256>::kDwords + kEl8Dwords;
         if (T == unsigned(TT))
             e = launch8_batch<DecBatchTag<TT>>(&k_ff8_dec_batch<TT, RB>, threads_for(TT, RB), objs, count, nunits, lds,
                                                s);

@@ -1,0 +1,295 @@
+"""GPU tier: library state over many threads and streams, the multi-GPU host
+fan-out, and the column-sharded path run by separate rank processes.
+
+* Scratch lifetime (include/leopard_amd.h, leo_amd_release_stream): the
+  reference holds no per-call state (SURVEY.md 8(b) "Ownership"); ours keeps
+  per (thread, device, stream) scratch, which must be bounded and freed when a
+  thread exits or a stream is released -- device memory returns to where it was.
+* Fan-out (leo_amd_set_fanout): a host-memory call split
+  into 64-byte-aligned column ranges, each coded by its own worker; the result
+  must equal the oracle whatever the split (ranges need not be equal).
+* Rank processes: two spawned processes share the one GPU,
+  each codes its column range of the object through leo_amd_*_slice; the union
+  carries the reference library's digests.
+"""
+import hashlib
+import json
+import os
+import socket
+import threading
+
+import numpy as np
+import pytest
+
+import oracle_lib as ol
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+MiB = 1 << 20
+
+
+def _free_mem():
+    torch.cuda.synchronize()
+    return torch.cuda.mem_get_info()[0]
+
+
+def _decode_case(k=1000, r=200, b=4096, seed=3):
+    rng = np.random.default_rng(seed)
+    data = rng.integers(0, 256, (k, b), dtype=np.uint8)
+    rec = ol.oracle().encode(data, r)
+    lost = sorted(rng.choice(k, r, replace=False).tolist())
+    return data, rec, lost
+
+
+def _device_decode(leo, d_data, d_rec, lost, work):
+    k, b = d_data.shape
+    r = d_rec.shape[0]
+    los = set(lost)
+    res = leo.leo_decode(b, k, r, work.shape[0], [None if i in los else d_data[i].data_ptr() for i in range(k)],
+                         [d_rec[i].data_ptr() for i in range(r)], [work[i].data_ptr() for i in range(work.shape[0])])
+    return res
+
+
+def test_scratch_freed_when_threads_exit(leo):
+    """50 short-lived threads each run a 1000+200 decode (GF(2^16): device arena,
+    decoder state, pinned staging); after they exit, device memory is back."""
+    data, rec, lost = _decode_case()
+    d_data, d_rec = torch.from_numpy(data).cuda(), torch.from_numpy(rec).cuda()
+    k, b = data.shape
+    wc = leo.leo_decode_work_count(k, rec.shape[0])
+    works = [torch.zeros((wc, b), dtype=torch.uint8, device="cuda") for _ in range(50)]
+    base = _free_mem()
+    results = [None] * 50
+
+    def run(j):
+        results[j] = _device_decode(leo, d_data, d_rec, lost, works[j])
+
+    for wave in range(5):  # 10 threads at a time
+        ts = [threading.Thread(target=run, args=(wave * 10 + t,)) for t in range(10)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+    assert all(r == leo.LeopardResult.Success for r in results), (results, leo.last_error())
+    for w in works:
+        for i in lost:
+            assert torch.equal(w[i], d_data[i])
+    assert base - _free_mem() <= 8 * MiB, "device memory not returned after the threads exited"
+
+
+def test_scratch_bounded_over_fresh_streams(leo):
+    """50 fresh streams on one thread: at most 8 scratch sets are kept (least
+    recently used freed first), and leo_amd_release_stream returns the rest."""
+    data, rec, lost = _decode_case(seed=4)
+    d_data, d_rec = torch.from_numpy(data).cuda(), torch.from_numpy(rec).cuda()
+    k, b = data.shape
+    wc = leo.leo_decode_work_count(k, rec.shape[0])
+    work = torch.zeros((wc, b), dtype=torch.uint8, device="cuda")
+    leo.release_stream(-1)
+    base = _free_mem()
+    one = peak = 0
+    try:
+        for j in range(50):
+            s = torch.cuda.Stream()
+            leo.set_stream(s.cuda_stream)
+            work.zero_()
+            torch.cuda.synchronize()
+            assert _device_decode(leo, d_data, d_rec, lost, work) == leo.LeopardResult.Success, leo.last_error()
+            s.synchronize()
+            for i in lost:
+                assert torch.equal(work[i], d_data[i]), (j, i)
+            used = base - _free_mem()
+            one = one or used  # one stream's scratch
+            peak = max(peak, used)
+            if j % 2:  # every other stream is released by the caller before it goes away
+                leo.release_stream(s.cuda_stream)
+            del s
+        assert peak <= 9 * one + 8 * MiB, (peak, one)  # at most 8 kept, whatever the number of streams
+    finally:
+        leo.set_stream(None)
+        leo.release_stream(-1)
+    assert base - _free_mem() <= 8 * MiB, "device memory not returned by leo_amd_release_stream"
+
+
+def test_async_calls_then_release_wait_for_the_work(leo):
+    """Release right after async calls: the scratch is freed only after the
+    queued kernels that read it are done (results stay correct)."""
+    data, rec, lost = _decode_case(k=600, r=300, b=8192, seed=5)
+    d_data, d_rec = torch.from_numpy(data).cuda(), torch.from_numpy(rec).cuda()
+    k, b = data.shape
+    wc = leo.leo_decode_work_count(k, rec.shape[0])
+    s = torch.cuda.Stream()
+    works = [torch.zeros((wc, b), dtype=torch.uint8, device="cuda") for _ in range(4)]
+    torch.cuda.synchronize()
+    leo.set_stream(s.cuda_stream)
+    leo.set_async(True)
+    try:
+        for w in works:
+            assert _device_decode(leo, d_data, d_rec, lost, w) == leo.LeopardResult.Success
+        leo.release_stream(s.cuda_stream)
+        s.synchronize()
+    finally:
+        leo.set_async(False)
+        leo.set_stream(None)
+    for w in works:
+        for i in lost:
+            assert torch.equal(w[i], d_data[i])
+
+
+# ------------------------------------------------------------------ fan-out --
+
+FANOUT_CASES = [  # (K, R, B, losses): B is not a multiple of 64 x ranges
+    (128, 128, 64 * 1001, 128), (100, 30, 64 * 333, 17), (1000, 200, 64 * 517, 200), (300, 300, 64 * 129, 300),
+]
+
+
+@pytest.mark.parametrize("ranges", [2, 3, 4, -1])
+@pytest.mark.parametrize("k,r,b,loss", FANOUT_CASES)
+def test_host_fanout_matches_oracle(leo, k, r, b, loss, ranges):
+    rng = np.random.default_rng(k * 7 + b + ranges)
+    data = rng.integers(0, 256, (k, b), dtype=np.uint8)
+    expect = ol.oracle().encode(data, r)
+    wc, dwc = leo.leo_encode_work_count(k, r), leo.leo_decode_work_count(k, r)
+    work = np.zeros((wc, b), dtype=np.uint8)
+    leo.set_fanout(ranges)
+    try:
+        res = leo.leo_encode(b, k, r, wc, [data[i].ctypes.data for i in range(k)],
+                             [work[i].ctypes.data for i in range(wc)])
+        assert res == leo.LeopardResult.Success, leo.last_error()
+        assert np.array_equal(work[:r], expect)
+        lost_o = sorted(rng.choice(k, loss, replace=False).tolist())
+        lost_r = sorted(rng.choice(r, r - loss, replace=False).tolist())
+        los, lrs = set(lost_o), set(lost_r)
+        dwork = np.zeros((dwc, b), dtype=np.uint8)
+        res = leo.leo_decode(b, k, r, dwc, [None if i in los else data[i].ctypes.data for i in range(k)],
+                             [None if i in lrs else expect[i].ctypes.data for i in range(r)],
+                             [dwork[i].ctypes.data for i in range(dwc)])
+        assert res == leo.LeopardResult.Success, leo.last_error()
+        for i in lost_o:
+            assert np.array_equal(dwork[i], data[i]), i
+    finally:
+        leo.set_fanout(0)
+
+
+def test_host_fanout_worker_error_reaches_caller(leo):
+    """A failure inside a fan-out worker comes back as the caller's result and
+    last_error: a lost original without a work piece is checked per column
+    range, i.e. on the workers of a fanned-out call."""
+    k, r, b = 20, 10, 64 * 40
+    data = np.zeros((k, b), dtype=np.uint8)
+    rec = ol.oracle().encode(data, r)
+    dwc = leo.leo_decode_work_count(k, r)
+    dwork = np.zeros((dwc, b), dtype=np.uint8)
+    pw = [dwork[i].ctypes.data for i in range(dwc)]
+    pw[3] = None  # lost original 3 has no output buffer
+    for ranges in (2, 0):
+        leo.set_fanout(ranges)
+        try:
+            res = leo.leo_decode(b, k, r, dwc, [None if i == 3 else data[i].ctypes.data for i in range(k)],
+                                 [rec[i].ctypes.data for i in range(r)], pw)
+        finally:
+            leo.set_fanout(0)
+        assert res == leo.LeopardResult.InvalidInput, (ranges, res)
+        assert "work_data[3]" in leo.last_error(), leo.last_error()
+
+
+# ----------------------------------------------------- rank processes ------
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _rank_main(rank, world, port, shared, results):
+    """One rank: its column range of each object through leo_amd_*_slice
+    (leopard_amd.sharding), on the one GPU both ranks share; gloo carries only
+    the barrier and the max of the elapsed times (no data-path collective).
+    The rank copies its columns of the outputs into the test's shared host
+    tensors (the test-side gather)."""
+    import sys
+    import time
+    import torch as th
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = {}
+    try:
+        import oracle_lib as olr
+        import leopard_amd as leo
+        from leopard_amd.sharding import decode_shard, encode_shard, max_over_ranks, shard_for_rank
+        th.cuda.set_device(0)
+        assert leo.leo_init() == 0, leo.last_error()
+        for (k, r, b) in [(1000, 200, 65536), (32768, 32768, 65536)]:
+            off, size = shard_for_rank(b, rank, world)
+            data = olr.hash_bytes_torch(7, k, b, "cuda")
+            wc, dwc = leo.leo_encode_work_count(k, r), leo.leo_decode_work_count(k, r)
+            work = th.empty((wc, b), dtype=th.uint8, device="cuda")
+            po = [data[i].data_ptr() for i in range(k)]
+            pw = [work[i].data_ptr() for i in range(wc)]
+            dist.barrier()
+            t0 = time.perf_counter()
+            assert encode_shard(b, rank, world, k, r, po, pw) == 0, leo.last_error()
+            th.cuda.synchronize()
+            el = max_over_ranks(time.perf_counter() - t0)
+            shared[f"rec_{k}"][:, off:off + size].copy_(work[:r, off:off + size].cpu())
+            dwork = th.empty((dwc, b), dtype=th.uint8, device="cuda")
+            pd = [dwork[i].data_ptr() for i in range(dwc)]
+            pr = [work[i].data_ptr() for i in range(r)]
+            if k == r:  # full loss of the originals: rebuilt exactly
+                assert decode_shard(b, rank, world, k, r, [None] * k, pr, pd) == 0, leo.last_error()
+                th.cuda.synchronize()
+                ok = bool(th.equal(dwork[:k, off:off + size], data[:, off:off + size]))
+            else:  # the decoder's exact map on non-codeword input (reference decode digest)
+                junk = olr.hash_bytes_torch(8, r, b, "cuda")
+                lo, lr = olr.benchmark_losses(k, r, r, seed=2, trial=0)
+                los, lrs = set(lo), set(lr)
+                assert decode_shard(b, rank, world, k, r, [None if i in los else po[i] for i in range(k)],
+                                    [None if i in lrs else junk[i].data_ptr() for i in range(r)], pd) == 0
+                th.cuda.synchronize()
+                idx = th.tensor(lo, device="cuda")
+                shared[f"dec_{k}"][:, off:off + size].copy_(dwork.index_select(0, idx)[:, off:off + size].cpu())
+                ok = True
+            out[k] = (ok, el)
+            del data, work, dwork
+            th.cuda.empty_cache()
+        results.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.slow
+def test_two_rank_processes_share_the_gpu_sliced(leo):
+    import torch.multiprocessing as mp
+    with open(os.path.join(GOLDEN, "golden_digests.json")) as f:
+        dig = json.load(f)
+    shared = {"rec_1000": torch.zeros((200, 65536), dtype=torch.uint8).share_memory_(),
+              "dec_1000": torch.zeros((200, 65536), dtype=torch.uint8).share_memory_(),
+              "rec_32768": torch.zeros((32768, 65536), dtype=torch.uint8).share_memory_()}
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(rk, 2, port, shared, q)) for rk in range(2)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(2):
+        rank, out = q.get(timeout=110)
+        got[rank] = out
+    for p in procs:
+        p.join(timeout=30)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    for rank in (0, 1):
+        assert got[rank][1000][0] and got[rank][32768][0], got
+        assert got[rank][32768][1] == got[1 - rank][32768][1]  # max over ranks agrees
+    sha = lambda t: hashlib.sha256(t.numpy().tobytes()).hexdigest()  # noqa: E731
+    assert sha(shared["rec_1000"]) == dig["hash_digests"]["1000_200_65536"]
+    assert sha(shared["dec_1000"]) == dig["decode_hash_digests"]["1000_200_65536"]
+    assert sha(shared["rec_32768"]) == dig["hash_digests"]["32768_32768_65536"]

@@ -408,23 +408,34 @@ LDEV void fwht256_mod255(unsigned (&e)[4], unsigned lane) {
     e[1] = Mod8::add(a1, a3);
     e[3] = Mod8::sub(a1, a3);
 }
-LDEV void error_locator8(const Ff8DecArgs& a, uint8_t* el, unsigned wave, unsigned lane) {
-    if (wave != 0) return;
-    unsigned e[4];
+// load(): the LogWalsh entries of wave 0's positions, issued at kernel start,
+// ahead of the piece loads (vmcnt retires in order: waiting for these then does
+// not wait for the pieces); run(): the two transforms, then el -> LDS.
+struct ErrorLocator8 {
+    unsigned w[4];
+    LDEV void load(const Ff8DecArgs& a, unsigned wave, unsigned lane) {
+        if (wave != 0) return;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const unsigned p = lane + 64u * j;
-        e[j] = (cload(a.erased + (p >> 5)) >> (p & 31)) & 1u;
+        for (int j = 0; j < 4; ++j) w[j] = a.walsh[lane + 64u * j];
     }
-    if constexpr ((LAMD_ABLATE & 32) == 0) {
-        fwht256_mod255(e, lane);
+    LDEV void run(const Ff8DecArgs& a, uint8_t* el, unsigned wave, unsigned lane) {
+        if (wave != 0) return;
+        unsigned e[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) e[j] = (e[j] * a.walsh[lane + 64u * j]) % 255u;
-        fwht256_mod255(e, lane);
+        for (int j = 0; j < 4; ++j) {
+            const unsigned p = lane + 64u * j;
+            e[j] = (cload(a.erased + (p >> 5)) >> (p & 31)) & 1u;
+        }
+        if constexpr ((LAMD_ABLATE & 32) == 0) {
+            fwht256_mod255(e, lane);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) e[j] = (e[j] * w[j]) % 255u;
+            fwht256_mod255(e, lane);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) el[lane + 64u * j] = uint8_t(e[j]);
     }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) el[lane + 64u * j] = uint8_t(e[j]);
-}
+};
 
 // v[r] *= table(log_of(r)) for the pieces with pred(r): the tables of KB pieces
 // are read together, then their multiplies run (one LDS round trip per batch).
@@ -458,6 +469,8 @@ LDEV void ff8_dec(const Ff8DecArgs& a) {
     sk_stage.load(a.sktab);
     log_stage.load(a.tabs);
     const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    ErrorLocator8 elc;
+    elc.load(a, w, lane);
     const Cols cl = strip_cols(a.nunits, lane);
     const PieceSpace ps{0, 0, 0};
     const Pyr8Live present{a.present}, needed{a.needed};
@@ -472,7 +485,7 @@ LDEV void ff8_dec(const Ff8DecArgs& a) {
         for (int r = 0; r < TL::NR; ++r) v[r][0] = present(pos(r), 0) ? gload(pp[r], cl) : 0u;
     }
     STAMP(1);
-    error_locator8(a, el, w, lane);
+    elc.run(a, el, w, lane);
     sk_stage.store(sk);
     log_stage.store(ltab);
     __syncthreads();
@@ -547,6 +560,8 @@ LDEV void ff8_dec_half(const Ff8DecArgs& a) {
     sk_stage.load(a.sktab);
     log_stage.load(a.tabs);
     const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    ErrorLocator8 elc;
+    elc.load(a, w, lane);
     const Cols cl = strip_cols(a.nunits, lane);
     const PieceSpace low{0, 0, 0}, high{0, 0, m};
     auto pyr = [](const uint32_t* w) {
@@ -563,7 +578,7 @@ LDEV void ff8_dec_half(const Ff8DecArgs& a) {
 #pragma unroll
         for (int r = 0; r < TL::NR; ++r) v[r][0] = present(lpos(r), 0) ? gload(pp[r], cl) : 0u;
     }
-    error_locator8(a, el, w, lane);
+    elc.run(a, el, w, lane);
     sk_stage.store(sk);
     log_stage.store(ltab);
     __syncthreads();
@@ -621,6 +636,8 @@ LDEV void ff8_dec_split(const Ff8DecArgs& a) {
     sk_stage.load(a.sktab);
     log_stage.load(a.tabs);
     const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    ErrorLocator8 elc;
+    elc.load(a, w, lane);
     const Cols cl = strip_cols(a.nunits, lane);
     const PieceSpace low{0, 0, 0}, high{0, 0, m};
     const Pyr8Live present{a.present}, needed{a.needed};
@@ -636,7 +653,7 @@ LDEV void ff8_dec_split(const Ff8DecArgs& a) {
 #pragma unroll
         for (int r = 0; r < TL::NR; ++r) x[r][0] = present(lpos(r), 0) ? gload(pp[r], cl) : 0u;
     }
-    error_locator8(a, el, w, lane);
+    elc.run(a, el, w, lane);
     sk_stage.store(sk);
     log_stage.store(ltab);
     __syncthreads();

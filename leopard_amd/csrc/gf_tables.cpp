@@ -183,4 +183,61 @@ void build_fused_top_logs16(const GaloisField& f, std::vector<uint32_t>& out) {
     }
 }
 
+// The high part Q = F_hi (I + D_hi) I_hi of the FF16 decoder transform over the
+// tiles of 256 positions (rs_ff16_small.hip), n = 256 * 2^H: the decoder's
+// skews (base -1) of the high layers depend on the tile index alone, so Q is
+// one 2^H x 2^H matrix over the field, applied to the unit vectors here with
+// the reference's butterflies (IFFT_DIT2 / FFT_DIT2, LeopardFF16.cpp:629-705,
+// 1083-1159; formal derivative :1738-1758 restricted to the high bits).  It is
+// an XOR-convolution, Q[t][t'] = q[t ^ t'], which is checked; returns false
+// (and leaves the narrow decoder off) if it were not.
+bool build_high_q16(const GaloisField& f, std::vector<uint32_t>& out) {
+    out.assign(kHighQ16Entries, kHighQZero);
+    const unsigned one = f.exp_of[0];
+    for (unsigned H = 1; H <= 3; ++H) {
+        const unsigned N = 1u << H;
+        std::vector<std::vector<unsigned>> Q(N, std::vector<unsigned>(N, 0));
+        for (unsigned tp = 0; tp < N; ++tp) {
+            std::vector<unsigned> v(N, 0);
+            v[tp] = one;
+            auto skew_of = [&](unsigned i, unsigned l) {
+                const unsigned p = i << 8;
+                return unsigned(f.skew[(((p >> l) | 1u) << l) - 1]);
+            };
+            for (unsigned b = 0; b < H; ++b) {  // IFFT, high layers bottom-up
+                const unsigned d = 1u << b;
+                for (unsigned i = 0; i < N; ++i) {
+                    if (i & d) continue;
+                    const unsigned lm = skew_of(i, 8 + b);
+                    v[i + d] ^= v[i];
+                    if (lm != f.modulus()) v[i] ^= f.mul_log(v[i + d], lm);
+                }
+            }
+            std::vector<unsigned> o(v);  // formal derivative on the high bits (sources unmodified)
+            for (unsigned k = 0; k < N; ++k)
+                for (unsigned b = 0; b < H; ++b)
+                    if (!((k >> b) & 1u)) o[k] ^= v[k | (1u << b)];
+            v = o;
+            for (unsigned b = H; b-- > 0;) {  // FFT, high layers top-down
+                const unsigned d = 1u << b;
+                for (unsigned i = 0; i < N; ++i) {
+                    if (i & d) continue;
+                    const unsigned lm = skew_of(i, 8 + b);
+                    if (lm != f.modulus()) v[i] ^= f.mul_log(v[i + d], lm);
+                    v[i + d] ^= v[i];
+                }
+            }
+            for (unsigned t = 0; t < N; ++t) Q[t][tp] = v[t];
+        }
+        for (unsigned t = 0; t < N; ++t)
+            for (unsigned tp = 0; tp < N; ++tp)
+                if (Q[t][tp] != Q[t ^ tp][0]) return false;
+        for (unsigned k = 0; k < N; ++k) {
+            const unsigned q = Q[k][0];
+            out[high_q16_base(H) + k] = q == 0 ? kHighQZero : q == one ? kHighQOne : unsigned(f.log_of[q]);
+        }
+    }
+    return true;
+}
+
 }  // namespace lamd

@@ -92,4 +92,12 @@ constexpr unsigned kFused16Entries = 65536;
 constexpr unsigned fused16_base(unsigned T) { return 65536u - (131072u >> T); }
 void build_fused_top_logs16(const GaloisField& f, std::vector<uint32_t>& out);
 
+// FF16 decoder, n = 256 * 2^H (H = 1..3): the high part of the transform as
+// q[t ^ t'] over tile indices (rs_ff16_small.hip), entry high_q16_base(H) + k:
+// the log value of q[k], or kHighQZero / kHighQOne.
+constexpr unsigned kHighQ16Entries = 14;
+constexpr uint32_t kHighQZero = 0xFFFFFFFFu, kHighQOne = 0xFFFFFFFEu;
+constexpr unsigned high_q16_base(unsigned H) { return (1u << H) - 2; }
+bool build_high_q16(const GaloisField& f, std::vector<uint32_t>& out);
+
 }  // namespace lamd

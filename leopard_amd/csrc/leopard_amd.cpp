@@ -81,6 +81,7 @@ struct DeviceTables {
     uint32_t* fused16 = nullptr;  // fused top-layer table indices of the FF16 encoders
     uint32_t* walsh8 = nullptr;
     uint32_t* walsh16 = nullptr;
+    uint32_t* qlog16 = nullptr;  // high part of the small FF16 decoder (gf_tables.h: build_high_q16)
     uint8_t* zeros = nullptr;   // zero page
     hipStream_t svc = nullptr;  // library-owned stream for releasing workspace memory
     bool ready = false;
@@ -90,7 +91,9 @@ std::mutex g_mu;
 bool g_initialized = false;
 int g_device_count = 0;
 std::vector<DeviceTables> g_dev;
-std::vector<uint32_t> g_h_tab8, g_h_tab16, g_h_sktab8, g_h_sktab16, g_h_fused8, g_h_fused16, g_h_walsh8, g_h_walsh16;
+std::vector<uint32_t> g_h_tab8, g_h_tab16, g_h_sktab8, g_h_sktab16, g_h_fused8, g_h_fused16, g_h_walsh8, g_h_walsh16,
+    g_h_qlog16;
+bool g_q16_ok = false;  // the high part is an XOR-convolution (always; checked at init)
 
 template <class T>
 hipError_t upload(T** dst, const std::vector<T>& src) {
@@ -115,6 +118,7 @@ LeopardResult ensure_device(int dev, DeviceTables** out) {
         HIP_OK(upload(&d.fused16, g_h_fused16), "upload FF16 fused indices");
         HIP_OK(upload(&d.walsh8, g_h_walsh8), "upload FF8 LogWalsh");
         HIP_OK(upload(&d.walsh16, g_h_walsh16), "upload FF16 LogWalsh");
+        HIP_OK(upload(&d.qlog16, g_h_qlog16), "upload FF16 high-part table");
         HIP_OK(hipMalloc(reinterpret_cast<void**>(&d.zeros), 4096), "zero page");
         HIP_OK(hipMemset(d.zeros, 0, 4096), "zero page");
         HIP_OK(hipStreamCreateWithFlags(&d.svc, hipStreamNonBlocking), "service stream");
@@ -449,6 +453,10 @@ struct MapBuilder {
     }
 };
 
+// Pieces of at most this many bytes count as narrow columns for the small
+// GF(2^16) kernels (rs_ff16_small.hip): 256 KiB = 2048 strips of 128 bytes.
+constexpr uint64_t kNarrowColumnsMax = 256 << 10;
+
 // Columns per GF(2^8) launch: its argument block counts dword columns in 32 bits.
 constexpr uint64_t kFf8MaxLaunchBytes = 1ull << 32;
 
@@ -552,8 +560,11 @@ LeopardResult encode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
     // on narrow columns, where the single-tile kernel's one workgroup per
     // 512-byte strip leaves CUs idle: pass 1 runs the chunk IFFTs in parallel
     // workgroups and pass 3 combines them (no high pass).
-    const bool chunk_parallel = ff16 && Tm == kLoBits && nchunks > 1 && bytes / 8 < 1024 * 64;
-    const bool multipass = (ff16 && Tm > kLoBits) || chunk_parallel;
+    // Narrow columns with m <= 256: one workgroup per 128-byte strip runs the
+    // whole encode (rs_ff16_small.hip), enough workgroups to fill the GPU.
+    const bool narrow = ff16 && encode16_small_supported(Tm) && bytes <= kNarrowColumnsMax;
+    const bool chunk_parallel = !narrow && ff16 && Tm == kLoBits && nchunks > 1 && bytes / 8 < 1024 * 64;
+    const bool multipass = !narrow && ((ff16 && Tm > kLoBits) || chunk_parallel);
     uint64_t slice = bytes, slab_bytes = 0;
     if (multipass) {
         const uint64_t slab_pieces = uint64_t(nchunks) * m + m;
@@ -566,6 +577,11 @@ LeopardResult encode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
     r = mb.flush(*c.ws, reinterpret_cast<uint64_t*>(c.ws->dbuf), c.s);
     if (r != Leopard_Success) return r;
 
+    if (narrow) {
+        a.nunits = bytes / unit_bytes;
+        HIP_OK(launch_encode16_small(Tm, a, c.s), "encode kernel");
+        return Leopard_Success;
+    }
     if (!multipass) {
         a.nunits = bytes / unit_bytes;
         HIP_OK(launch_encode_fused16(Tm, a, c.s), "encode kernel");
@@ -807,8 +823,12 @@ LeopardResult decode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
     std::copy(erased.begin(), erased.end(), key.begin() + 2);
     const bool rebuild = key != ws.dec16_key;
 
-    const uint64_t slab_pieces = 2ull * n;  // U (pass 1 -> 2, 3) and A (pass 2 -> 3)
-    const uint64_t slice = mall_slice(bytes, slab_pieces);
+    // Narrow columns and n <= 2048: the two-pass narrow-strip decoder
+    // (rs_ff16_small.hip), whose only intermediate is U (tiles with received data).
+    const unsigned ntiles_in = (m + K + (1u << kLoBits) - 1) >> kLoBits;
+    const bool narrow = g_q16_ok && decode16_small_supported(Tn) && bytes <= kNarrowColumnsMax;
+    const uint64_t slab_pieces = narrow ? uint64_t(ntiles_in) << kLoBits : 2ull * n;  // U (+ A, multi-pass)
+    const uint64_t slice = narrow ? bytes : mall_slice(bytes, slab_pieces);
     const size_t table_bytes = (mb.bytes() + 255) / 256 * 256;
     const size_t off_slab = table_bytes;
     LeopardResult r = ws.reserve_device(off_slab + slab_pieces * slice);
@@ -863,6 +883,17 @@ LeopardResult decode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
         a.fused = c.t->fused16 + fused16_base(Tn - 1);
     }
 
+    if (narrow) {
+        a.nlo = ntiles_in;
+        a.qlog = c.t->qlog16 + high_q16_base(Tn - kLoBits);
+        a.tile0 = m >> kLoBits;
+        a.nout = ((m + K - 1) >> kLoBits) - a.tile0 + 1;
+        a.nunits = bytes / 8;
+        a.a_out = a.a_in = PieceMap{nullptr, ws.dbuf + off_slab, bytes, 0};
+        HIP_OK(launch_decode16_small_lo(a, c.s), "decode pass 1");
+        HIP_OK(launch_decode16_small_fin(a, c.s), "decode pass 2");
+        return Leopard_Success;
+    }
     uint8_t* A = ws.dbuf + off_slab;
     uint8_t* Uu = A + uint64_t(n) * slice;
     for (uint64_t pos = 0; pos < bytes; pos += slice) {
@@ -1730,6 +1761,7 @@ LEO_EXPORT int leo_init_(int version) {
     build_fused_top_logs16(f16, g_h_fused16);
     g_h_walsh8.assign(f8.log_walsh.begin(), f8.log_walsh.end());
     g_h_walsh16.assign(f16.log_walsh.begin(), f16.log_walsh.end());
+    g_q16_ok = build_high_q16(f16, g_h_qlog16);
     g_dev.assign(count, DeviceTables{});
     g_device_count = count;
     g_initialized = true;

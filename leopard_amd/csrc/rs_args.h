@@ -46,6 +46,11 @@ struct DecArgs {
     const uint32_t* reveal_logs; // FF16: log value of the reveal multiply per position
     unsigned K, R, m, Tn, nlo;   // nlo: number of non-zero low tiles
     uint64_t nunits;
+    // narrow-strip decoder (n <= 2048, rs_ff16_small.hip): the high part of the
+    // transform as the matrix q[t ^ t'] over 256-position tiles (gf_tables.h:
+    // build_high_q16), and the tiles holding originals [tile0, tile0 + nout)
+    const uint32_t* qlog;
+    unsigned tile0, nout;
 };
 
 // GF(2^8) kernels (codeword length n <= 256).  Everything a launch needs travels
@@ -141,6 +146,15 @@ hipError_t launch_error_locator16(const uint32_t* erased, const uint32_t* walsh,
                                   uint32_t* scale_logs, uint32_t* reveal_logs, unsigned m, unsigned K, unsigned R,
                                   hipStream_t s);
 hipError_t launch_xor_reduce(const XorArgs& a, hipStream_t s);
+// Small GF(2^16) codes on narrow column strips (rs_ff16_small.hip)
+bool encode16_small_supported(unsigned Tm);
+hipError_t launch_encode16_small(unsigned Tm, const EncArgs& a, hipStream_t s);
+// decode, n = 2^Tn with 9 <= Tn <= 11: pass 1 (scale + low IFFT of every tile
+// with received data -> slab a_out), pass 2 (high part + D_lo + low FFT +
+// reveal of every tile holding a lost original, slab a_in = pass 1's)
+bool decode16_small_supported(unsigned Tn);
+hipError_t launch_decode16_small_lo(const DecArgs& a, hipStream_t s);
+hipError_t launch_decode16_small_fin(const DecArgs& a, hipStream_t s);
 hipError_t launch_ff8_encode(unsigned T, const Ff8EncArgs& a, hipStream_t s);
 hipError_t launch_ff8_decode(unsigned T, const Ff8DecArgs& a, hipStream_t s);
 // Batched GF(2^8) launches: `count` argument blocks in device memory (same T,

@@ -342,11 +342,19 @@ struct GlobalWindow {
 // ds_read_b128 at a wave-uniform address into VGPRs, so v_perm takes both
 // table dwords from VGPRs (SGPR tables cost a v_mov per perm pair) and no
 // scalar-load round trip sits in front of every butterfly group.
+//
+// Slot s starts at dword tab16_slot(s): 20 dwords a slot plus 4 dwords of
+// padding after every 8th and every 64th slot.  Lane groups that hold
+// different pieces (Tile LW < 64) read slots 8, 16, ... or 64, 128, ... apart
+// in the same instruction; without the padding those start in the same LDS
+// bank (20 * 8 = 160 = 0 mod 32 dwords) and the reads serialise.
+__host__ __device__ constexpr unsigned tab16_slot(unsigned s) { return 20u * s + 4u * ((s >> 3) + (s >> 6)); }
+constexpr size_t tab16_set_dwords(int T) { return tab16_slot(1u << T); }
 struct LdsWindow16 {
     const uint32_t* set;
     unsigned hi_fixed, l0;
     LDEV constexpr bool zero(unsigned) const { return false; }
-    LDEV FF16::Tab table(unsigned cidx) const { return FF16::tab_lds(set + ((cidx - hi_fixed) >> l0) * 20u); }
+    LDEV FF16::Tab table(unsigned cidx) const { return FF16::tab_lds(set + tab16_slot((cidx - hi_fixed) >> l0)); }
     LDEV void stage(const uint32_t*, int) {}
 };
 constexpr size_t kTab16LdsDwords = 20;
@@ -373,7 +381,8 @@ struct Tabs16Stage {
         static_for<0, int(PER)>([&](auto I) __attribute__((always_inline)) {
             constexpr unsigned i = decltype(I)::value;
             const unsigned e = threadIdx.x + i * NT;
-            if ((i + 1) * NT <= kVec || e < kVec) reinterpret_cast<uint4*>(set)[5 + e] = v[i];
+            const unsigned j = 1 + e / 5, k = e % 5;
+            if ((i + 1) * NT <= kVec || e < kVec) reinterpret_cast<uint4*>(set)[tab16_slot(j) / 4 + k] = v[i];
         });
     }
 };
@@ -395,11 +404,12 @@ struct LogTabs16Stage {
             v[i] = reinterpret_cast<const uint4*>(tabs)[size_t(lm) * 6 + e % 5];
         });
     }
+    // slot p (the table of logs[p]) at dword tab16_slot(p), as the skew sets
     LDEV void store(uint32_t* dst) const {
         static_for<0, int(PER)>([&](auto I) __attribute__((always_inline)) {
             constexpr unsigned i = decltype(I)::value;
             const unsigned e = threadIdx.x + i * NT;
-            if ((i + 1) * NT <= kVec || e < kVec) reinterpret_cast<uint4*>(dst)[e] = v[i];
+            if ((i + 1) * NT <= kVec || e < kVec) reinterpret_cast<uint4*>(dst)[tab16_slot(e / 5) / 4 + e % 5] = v[i];
         });
     }
 };
@@ -521,7 +531,14 @@ LDEV unsigned skew_index(unsigned i, unsigned l) { return ((i >> l) | 1u) << l; 
 #ifndef LAMD_FF8_KB
 #define LAMD_FF8_KB 4  // FF8 butterfly tables read (and live) together per layer batch
 #endif
-template <class F, int T, int R, int C, int LW = 64, int S = 0>
+// LGL: the lane group (LW < 64) is the low LGL bits of the virtual wave index
+// (0: no lane groups, or lane groups above the wave, as the GF(2^8) encoder's
+// lane-group forms).  In a layout whose low lo(k) >= LGL bits come from the
+// virtual wave, the lane groups then hold tile bits below every layer of that
+// layout, whose butterfly tables are therefore the same for all lane groups:
+// they are addressed from the wave-uniform part of the index (scalar address
+// arithmetic, no per-lane table addresses kept live).
+template <class F, int T, int R, int C, int LW = 64, int S = 0, int LGL = 0>
 struct Tile {
     static_assert(R >= 1 && R <= T, "register bits");
     static constexpr int NR = 1 << R;         // pieces per lane
@@ -596,10 +613,14 @@ struct Tile {
         constexpr int half = 1 << rb;
         const unsigned gl = ps.l0 + L;
         auto live = [&](int g) { return pred(ps.global(piece(LAY, g, w)), gl + 1); };
+        const unsigned wt = [&] {
+            if constexpr (LGL > 0 && LGL <= lo(LAY)) return uniform(w);  // lane 0 is lane group 0
+            else return w;
+        }();
         auto table = [&](int g) {
             // A zero skew has an all-zero table: the multiply-add adds 0, which is
             // the reference's XOR-only butterfly.
-            return win.table(skew_index(ps.global(piece(LAY, g, w)), gl));
+            return win.table(skew_index(ps.global(piece(LAY, g, wt)), gl));
         };
         auto zero = [&](int g) { return win.zero(skew_index(ps.global(piece(LAY, g, w)), gl)); };
         // XOR-only butterflies of a zero-skew group (wave-uniform branch): the

@@ -1,0 +1,404 @@
+// rs_ff16_small.hip -- GF(2^16) kernels for small codes (m <= 256 encode,
+// n <= 2048 decode) on narrow column strips, for gfx950.
+//
+// At 64 KiB pieces a 512-byte column strip per workgroup (the layout of
+// rs_kernels.hip) gives 128 strips: too few workgroups to fill 256 CUs, so the
+// small-code kernels there split the transform into slab passes and still leave
+// SIMDs idle.  Here a workgroup owns a strip of LW units (LW < 64: 16 units =
+// two 64-byte ALTMAP blocks = 128 bytes of every piece), and the 64 lanes of a
+// wave form 64 / LW lane groups that hold DIFFERENT pieces of the tile (Tile
+// LW, rs_device.h: the "virtual wave" index carries the lane-group bits).  So a
+// 64 KiB call is 512 workgroups, each running its whole transform:
+//   * butterfly tables are staged per workgroup in LDS (Tabs16Stage) and read
+//     at a per-lane address (a lane group's pieces sit in different butterfly
+//     groups: same ds_read_b128 count as a wave-uniform read);
+//   * piece pointers are per lane group (vector address arithmetic).
+//
+// Encoder (ReedSolomonEncode, LeopardFF16.cpp:1397-1467):
+//   work = XOR_c IFFT_m(data chunk c, skew base m - 1 + c m);  out = FFT_m(work, skew base -1)[0, R)
+// as one workgroup per strip looping over the chunks, the next chunk's pieces
+// loaded while the current chunk's IFFT runs; the top
+// IFFT layer of every chunk and the top FFT layer run as one fused butterfly
+// (Tile::fused_top, as rs_ff8.hip).
+#include <hip/hip_runtime.h>
+
+#include "rs_args.h"
+
+namespace lamd {
+
+#ifdef LAMD_STAMPS
+// Diagnostic builds only (tools/build_variant.sh ... -DLAMD_STAMPS): per-wave
+// s_memrealtime stamps at phase boundaries, without draining memory
+// operations (the prefetch overlap stays as it is).
+__device__ uint64_t* g_stamps16;
+#define STAMP16(k)                                                                                        \
+    do {                                                                                                 \
+        const uint64_t t_ = __builtin_amdgcn_s_memrealtime();                                            \
+        if ((threadIdx.x & 63) == 0)                                                                     \
+            g_stamps16[(uint64_t(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8 + (k)] = t_; \
+    } while (0)
+#else
+#define STAMP16(k) \
+    do {           \
+    } while (0)
+#endif
+
+namespace {
+
+// Units (8 bytes: 4 ALTMAP elements) of a lane: q = strip * LW + lane; byte
+// offset of unit q inside a piece (unit_offset<FF16>).
+template <int LW>
+struct NarrowCols {
+    uint64_t off;  // byte offset of this lane's unit (lanes past the end: the last unit)
+    bool live;
+};
+template <int LW>
+LDEV NarrowCols<LW> narrow_cols(uint64_t nunits, unsigned lane, uint64_t strip = blockIdx.x) {
+    const uint64_t q = strip * LW + lane;
+    const uint64_t ql = q < nunits ? q : nunits - 1;
+    return NarrowCols<LW>{unit_offset<FF16>(ql), q < nunits};
+}
+
+// Addresses of the pieces idx(r), r < NR, of a caller's map at per-lane
+// indices: one wave-uniform table-or-slab decision, every table entry read
+// before any piece load is issued (a table read in front of each piece load
+// would make each wait for all earlier loads: vmcnt retires in order).
+template <int NR, class Idx>
+LDEV void lane_ptrs(uint64_t (&pp)[NR], const PieceMap& pm, Idx idx) {
+    if (pm.table) {
+#pragma unroll
+        for (int r = 0; r < NR; ++r) pp[r] = pm.table[idx(r)];
+    } else {
+#pragma unroll
+        for (int r = 0; r < NR; ++r) pp[r] = uint64_t(reinterpret_cast<uintptr_t>(pm.base)) + uint64_t(idx(r)) * pm.stride;
+    }
+#pragma unroll
+    for (int r = 0; r < NR; ++r) pp[r] += pm.off;
+}
+LDEV void ld_unit(uint32_t* x, const uint8_t* piece, uint64_t off) {
+    x[0] = *gptr<const uint32_t>(piece + off);
+    x[1] = *gptr<const uint32_t>(piece + off + 32);
+}
+LDEV void st_unit(uint8_t* piece, uint64_t off, const uint32_t* x) {
+    *gptr<uint32_t>(piece + off) = x[0];
+    *gptr<uint32_t>(piece + off + 32) = x[1];
+}
+
+constexpr int lg_bits(int LW) { return LW == 64 ? 0 : LW == 32 ? 1 : LW == 16 ? 2 : 3; }
+template <int T, int R, int LW>
+constexpr unsigned threads_n() { return 64u << (T - R - lg_bits(LW)); }
+
+// ------------------------------------------------------------------ encode --
+
+template <int T, int R, int LW>
+__global__ void __launch_bounds__((threads_n<T, R, LW>()), 4) k_enc16n(EncArgs a) {
+    if constexpr ((LAMD_ABLATE & 16) != 0) return;
+    constexpr int G = lg_bits(LW);
+    static_assert(T - R - G >= 0, "at least one wave");
+    using TL = Tile<FF16, T, R, 1, LW, 0, G>;
+    constexpr unsigned NT = threads_n<T, R, LW>();
+    constexpr unsigned m = 1u << T;
+    constexpr size_t kSet = tab16_set_dwords(T);
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    auto set_of = [&](unsigned k) { return lds + TL::kXchDwords + (k & 1u) * kSet; };  // two table sets
+    const unsigned wave = uniform(threadIdx.x >> 6);
+    const unsigned lane = threadIdx.x & (LW - 1);
+    // virtual wave index: the lane group in its low bits.  In layout 0 the lane
+    // groups then hold tile bits R, R + 1 and in every later layout bits 0, 1:
+    // below every layer of those layouts, so their butterfly tables are the
+    // same for all lane groups (a layer on bit l uses the skew of the bits
+    // above l); only the layers of layout 0 read per-lane-group tables.
+    const unsigned w = (wave << G) | ((threadIdx.x & 63u) >> (6 - G));
+    const NarrowCols<LW> cl = narrow_cols<LW>(a.nunits, lane);
+    const PieceSpace ps{0, 0, 0};
+    typename TL::Reg x, nx, acc;
+    // chunk c's pieces base + tp (tp = tile piece of register r in layout 0).
+    // Branch-free: a piece past K re-reads piece K - 1 and is dropped at use
+    // (take_chunk), as the zero padding of the last chunk (LeopardFF16.cpp:1446-1448).
+    auto piece_of = [&](unsigned c, int r) { return c * m + TL::piece(0, r, w); };
+    auto load_chunk = [&](typename TL::Reg& dst, unsigned c, auto&& between) {
+        uint64_t pp[TL::NR];
+        lane_ptrs(pp, a.in, [&](int r) { return min(piece_of(c, r), a.K - 1); });
+        between();  // issued after the table reads, before the piece loads
+#pragma unroll
+        for (int r = 0; r < TL::NR; ++r) ld_unit(dst[r], reinterpret_cast<const uint8_t*>(pp[r]), cl.off);
+    };
+    auto take_chunk = [&](typename TL::Reg& dst, const typename TL::Reg& src, unsigned c) {
+#pragma unroll
+        for (int r = 0; r < TL::NR; ++r) {
+            const bool ok = piece_of(c, r) < a.K;
+#pragma unroll
+            for (int k = 0; k < TL::U; ++k) dst[r][k] = ok ? src[r][k] : 0u;
+        }
+    };
+    STAMP16(0);
+    {
+        Tabs16Stage<NT, T> st;
+        load_chunk(nx, 0, [&] { st.load(a.sktab, int(m - 1), 0, 0); });  // chunk 0's IFFT skews
+        st.store(set_of(0));
+        take_chunk(x, nx, 0);
+        __syncthreads();
+    }
+    STAMP16(1);
+    TL::zero(acc);
+    for (unsigned c = 0;;) {
+        const bool more = c + 1 < a.nchunks;
+        if (more)  // next chunk's pieces in flight during this chunk's transform
+            load_chunk(nx, c + 1, [] {});
+        // an opaque copy of w per chunk: the per-lane table addresses are
+        // recomputed in each chunk instead of being hoisted and kept live
+        unsigned wc = w;
+        asm volatile("" : "+v"(wc));
+        TL::template ifft<true>(x, wc, lane, lds, ps, LdsWindow16{set_of(c), 0, 0}, AllLive{});
+        TL::fused_top(x, FF16::tab(a.tabs, cload(a.fused + c)));
+        TL::xor_into(acc, x);
+        STAMP16(2 + (c < 3 ? c : 3));
+        if (!more) break;
+        ++c;
+        {
+            // its tables (L2-resident after the first workgroups: a short wait),
+            // into the set chunk c - 2 used (read before the previous barrier)
+            Tabs16Stage<NT, T> st;
+            st.load(a.sktab, int(m - 1 + c * m), 0, 0);
+            st.store(set_of(c));
+        }
+        take_chunk(x, nx, c);
+        __syncthreads();
+    }
+    {
+        // FFT tables (skew base -1) into the set the last chunk did not use
+        uint32_t* fset = set_of(a.nchunks);
+        Tabs16Stage<NT, T> st;
+        st.load(a.sktab, -1, 0, 0);
+        st.store(fset);
+        __syncthreads();
+        TL::template fft<true>(acc, w, lane, lds, ps, LdsWindow16{fset, 0, 0}, AllLive{});
+    }
+    TL::pin(acc);
+    STAMP16(6);
+    uint64_t pp[TL::NR];
+    lane_ptrs(pp, a.out, [&](int r) { return min(TL::piece(0, r, w), a.R - 1); });
+    if (!cl.live) return;
+#pragma unroll
+    for (int r = 0; r < TL::NR; ++r)
+        if (TL::piece(0, r, w) < a.R) st_unit(reinterpret_cast<uint8_t*>(pp[r]), cl.off, acc[r]);
+    STAMP16(7);
+}
+
+template <int T, int R, int LW>
+hipError_t launch_enc16n(const EncArgs& a, hipStream_t s) {
+    using TL = Tile<FF16, T, R, 1, LW, 0, lg_bits(LW)>;
+    constexpr size_t lds = (TL::kXchDwords + 2 * tab16_set_dwords(T)) * 4;
+    static_assert(lds <= 80 * 1024, "two workgroups per CU");
+    static hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_enc16n<T, R, LW>),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+    if (attr != hipSuccess) return attr;
+    void* params[] = {const_cast<EncArgs*>(&a)};
+    const unsigned grid = unsigned((a.nunits + LW - 1) / LW);
+    return hipLaunchKernel(reinterpret_cast<const void*>(&k_enc16n<T, R, LW>), dim3(grid), dim3(threads_n<T, R, LW>()),
+                           params, lds, s);
+}
+
+
+// ------------------------------------------------------------------ decode --
+//
+// Decoder (ReedSolomonDecode, LeopardFF16.cpp:1652-1775) for n = 2^Tn <= 2048:
+//   v = IFFT_n(el * received);  z = FormalDerivative(v);  lost i = FFT_n(z)[m + i] * exp(-el[m + i])
+// Positions split into tiles of 256 (low 8 bits) and Tn - 8 high bits t:
+//   F (I + D) I = F_lo ( Q + D_lo ) I_lo,    Q = F_hi (I + D_hi) I_hi
+// (D_lo commutes with the high layers, F_hi I_hi = I: rs_kernels.hip header).
+// Q acts on the tile index alone, the same for every low index; it is the
+// XOR-convolution Q[t][t'] = q[t ^ t'] with q[0] = 0, q[1] = 1 (gf_tables.h:
+// build_high_q16).  Hence two passes and one intermediate:
+//   pass 1 (k_dec16n_lo):  U_t' = IFFT_lo^(t')( el * received tile t' )            -> slab
+//   pass 2 (k_dec16n_fin): Z_t = XOR_t' q[t ^ t'] U_t'  ^  D_lo U_t,
+//                          lost originals of tile t = FFT_lo^(t)(Z_t) * exp(-el)
+// At 1000 + 200: 13 multiplies and 3 XORs per position for the high part (the
+// 3-pass form: 14 multiplies, plus a slab written and read).
+
+// bit j of level L of an occupancy pyramid (rs_args.h)
+LDEV bool pyr_bit(const uint32_t* pyr, unsigned L, unsigned j) {
+    return (cload(pyr + pyr_offset(L) + (j >> 5)) >> (j & 31)) & 1u;
+}
+constexpr uint32_t kQZero = 0xFFFFFFFFu, kQOne = 0xFFFFFFFEu;  // q entries that are 0 / 1 (else a log value)
+
+template <int R, int LW>
+__global__ void __launch_bounds__((threads_n<8, R, LW>()), 4) k_dec16n_lo(DecArgs a) {
+    if constexpr ((LAMD_ABLATE & 16) != 0) return;
+    constexpr int T = 8, G = lg_bits(LW);
+    using TL = Tile<FF16, T, R, 1, LW, 0, G>;
+    constexpr unsigned NT = threads_n<T, R, LW>();
+    const unsigned y = blockIdx.y;
+    if (!pyr_bit(a.present_pyr, T, y)) return;  // nothing received in this tile: U_y = 0, pass 2 skips it
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    uint32_t* set = lds + TL::kXchDwords;
+    uint32_t* scl = set + tab16_set_dwords(T);
+    const unsigned wave = uniform(threadIdx.x >> 6), lane = threadIdx.x & (LW - 1);
+    const unsigned w = (wave << G) | ((threadIdx.x & 63u) >> (6 - G));
+    const NarrowCols<LW> cl = narrow_cols<LW>(a.nunits, lane);
+    const PieceSpace ps{0, 0, y << T};
+    // erasure bits of this lane's pieces: in layout 0 a lane holds NR
+    // consecutive positions (tile piece r | w << R), all in one bitmap word
+    const uint32_t ew = a.erased_dev[(y << 3) + (w >> (5 - R))];
+    Tabs16Stage<NT, T> st;
+    LogTabs16Stage<NT, (1u << T)> ls;
+    st.load(a.sktab, -1, y << T, 0);
+    ls.load(a.tabs, a.scale_logs + (y << T));
+    typename TL::Reg x;
+    {
+        // received pieces: positions [0, R) recovery, [m, m + K) originals
+        // (LeopardFF16.cpp:1715-1730); absent ones read the zero page
+        auto pos = [&](int r) { return (y << T) + TL::piece(0, r, w); };
+        uint64_t pr[TL::NR], po[TL::NR];
+        lane_ptrs(pr, a.rec, [&](int r) { return min(pos(r), a.R - 1); });
+        lane_ptrs(po, a.orig, [&](int r) { return pos(r) >= a.m ? min(pos(r) - a.m, a.K - 1) : 0u; });
+#pragma unroll
+        for (int r = 0; r < TL::NR; ++r) {
+            const unsigned p = pos(r), tp = TL::piece(0, r, w);
+            const bool got = !((ew >> (tp & 31)) & 1u) && (p < a.R || (p >= a.m && p < a.m + a.K));
+            const uint8_t* src = got ? reinterpret_cast<const uint8_t*>(p < a.R ? pr[r] : po[r]) : a.zeros;
+            ld_unit(x[r], src, got ? cl.off : (cl.off & 31));
+        }
+    }
+    st.store(set);
+    ls.store(scl);
+    __syncthreads();
+    // scale by exp(el[p]) (the zero table for absent positions)
+#pragma unroll
+    for (int r = 0; r < TL::NR; ++r) {
+        asm volatile("" ::: "memory");  // one table live at a time
+        const FF16::Tab t = FF16::tab_lds(scl + tab16_slot(TL::piece(0, r, w)));
+        FF16::mul(x[r], x[r], t);
+#pragma unroll
+        for (int k = 0; k < TL::U; ++k) asm volatile("" : "+v"(x[r][k]));
+    }
+    TL::ifft(x, w, lane, lds, ps, LdsWindow16{set, y << T, 0}, AllLive{});
+    if (!cl.live) return;
+#pragma unroll
+    for (int r = 0; r < TL::NR; ++r) {
+        const uint64_t row = ps.global(TL::piece(TL::kLast, r, w));
+        st_unit(a.a_out.base + row * a.a_out.stride + a.a_out.off, cl.off, x[r]);
+    }
+}
+
+template <int R, int LW>
+__global__ void __launch_bounds__((threads_n<8, R, LW>()), 4) k_dec16n_fin(DecArgs a) {
+    if constexpr ((LAMD_ABLATE & 16) != 0) return;
+    constexpr int T = 8, G = lg_bits(LW);
+    using TL = Tile<FF16, T, R, 1, LW, 0, G>;
+    constexpr unsigned NT = threads_n<T, R, LW>();
+    // workgroup i runs on XCD i % 8: the nout workgroups of one strip (its
+    // output tiles) are dealt to one XCD back to back, so the U tiles they all
+    // read come from that XCD's L2
+    const unsigned j = blockIdx.x >> 3;
+    const uint64_t strip = (blockIdx.x & 7u) + 8ull * (j / a.nout);
+    const unsigned t = a.tile0 + j % a.nout;
+    if (strip * LW >= a.nunits) return;
+    if (!pyr_bit(a.needed_pyr, T, t)) return;  // no lost original in tile t
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    uint32_t* fset = lds + TL::kXchDwords;
+    uint32_t* rvl = fset + tab16_set_dwords(T);
+    const unsigned wave = uniform(threadIdx.x >> 6), lane = threadIdx.x & (LW - 1);
+    const unsigned w = (wave << G) | ((threadIdx.x & 63u) >> (6 - G));
+    const NarrowCols<LW> cl = narrow_cols<LW>(a.nunits, lane, strip);
+    const uint32_t ew = a.erased_dev[(t << 3) + (w >> (5 - R))];  // layout 0: one word a lane
+    Tabs16Stage<NT, T> st;
+    LogTabs16Stage<NT, (1u << T)> ls;
+    st.load(a.sktab, -1, t << T, 0);
+    ls.load(a.tabs, a.reveal_logs + (t << T));
+    // U tile u (layout kLast: the layout the low IFFT ended in and the FFT starts in)
+    auto load_u = [&](typename TL::Reg& u, unsigned ut) {
+#pragma unroll
+        for (int r = 0; r < TL::NR; ++r) {
+            const uint64_t row = (ut << T) + TL::piece(TL::kLast, r, w);
+            ld_unit(u[r], a.a_in.base + row * a.a_in.stride + a.a_in.off, cl.off);
+        }
+    };
+    st.store(fset);
+    ls.store(rvl);
+    __syncthreads();
+    typename TL::Reg z;
+    TL::zero(z);
+    for (unsigned ut = 0; ut < a.nlo; ++ut) {
+        if (!pyr_bit(a.present_pyr, T, ut)) continue;  // U = 0 (workgroup-uniform)
+        const uint32_t q = cload(a.qlog + (t ^ ut));
+        if (q == kQZero && ut != t) continue;
+        typename TL::Reg u;
+        load_u(u, ut);
+        if (q == kQOne) {
+            TL::xor_into(z, u);
+        } else if (q != kQZero) {
+            const FF16::Tab tq = FF16::tab(a.tabs, q);
+#pragma unroll
+            for (int r = 0; r < TL::NR; ++r) {
+                FF16::muladd(z[r], u[r], tq);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        // the formal derivative's low bits: D_lo U_t (rs_device.h derivative_add)
+        if (ut == t)
+            TL::derivative_add(z, [&](int r, uint32_t* out) { out[0] = u[r][0]; out[1] = u[r][1]; }, w, lane, lds);
+    }
+    TL::fft(z, w, lane, lds, PieceSpace{0, 0, t << T}, LdsWindow16{fset, t << T, 0}, AllLive{});
+    // lost original at p = m + i: work[i] = z[p] * exp(-el[p])  (LeopardFF16.cpp:1771-1773)
+    auto pos = [&](int r) { return (t << T) + TL::piece(0, r, w); };
+    uint64_t po[TL::NR];
+    lane_ptrs(po, a.out, [&](int r) { return pos(r) >= a.m ? min(pos(r) - a.m, a.K - 1) : 0u; });
+    if (!cl.live) return;
+#pragma unroll
+    for (int r = 0; r < TL::NR; ++r) {
+        const unsigned p = pos(r), tp = TL::piece(0, r, w);
+        if (p >= a.m && p < a.m + a.K && ((ew >> (tp & 31)) & 1u)) {
+            asm volatile("" ::: "memory");
+            uint32_t o[2];
+            FF16::mul(o, z[r], FF16::tab_lds(rvl + tab16_slot(tp)));
+            st_unit(reinterpret_cast<uint8_t*>(po[r]), cl.off, o);
+        }
+    }
+}
+
+template <class Kern>
+hipError_t launch16n(Kern* fn, dim3 grid, unsigned threads, size_t lds_bytes, const DecArgs& a, hipStream_t s) {
+    const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, int(lds_bytes));
+    if (attr != hipSuccess) return attr;
+    void* params[] = {const_cast<DecArgs*>(&a)};
+    return hipLaunchKernel(reinterpret_cast<const void*>(fn), grid, dim3(threads), params, lds_bytes, s);
+}
+
+constexpr int kDecR = 3, kDecLW = 16;
+using DecTL = Tile<FF16, 8, kDecR, 1, kDecLW, 0, lg_bits(kDecLW)>;
+constexpr size_t kDecLds = (DecTL::kXchDwords + tab16_set_dwords(8) + tab16_slot(256)) * 4;
+static_assert(kDecLds <= 80 * 1024, "two workgroups per CU");
+}  // namespace
+
+#ifdef LAMD_STAMPS
+extern "C" __attribute__((visibility("default"))) int leo_amd_debug_stamps16(void* buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps16), &buf, sizeof(buf)) == hipSuccess ? 0 : -1;
+}
+#endif
+
+// m = 2^Tm with Tm = 7, 8 (m = 128, 256), narrow strips of 16 units.
+bool encode16_small_supported(unsigned Tm) { return Tm == 7 || Tm == 8; }
+hipError_t launch_encode16_small(unsigned Tm, const EncArgs& a, hipStream_t s) {
+    switch (Tm) {
+        case 7: return launch_enc16n<7, 3, 16>(a, s);
+        case 8: return launch_enc16n<8, 3, 16>(a, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+// n = 2^Tn, 9 <= Tn <= 11 (2 .. 8 tiles of 256 positions)
+bool decode16_small_supported(unsigned Tn) { return Tn >= 9 && Tn <= 11; }
+hipError_t launch_decode16_small_lo(const DecArgs& a, hipStream_t s) {
+    const unsigned strips = unsigned((a.nunits + kDecLW - 1) / kDecLW);
+    return launch16n(&k_dec16n_lo<kDecR, kDecLW>, dim3(strips, a.nlo), threads_n<8, kDecR, kDecLW>(), kDecLds, a, s);
+}
+hipError_t launch_decode16_small_fin(const DecArgs& a, hipStream_t s) {
+    const unsigned strips = unsigned((a.nunits + kDecLW - 1) / kDecLW);
+    const unsigned groups = (strips + 7) / 8;  // strips dealt 8 at a time, one per XCD
+    return launch16n(&k_dec16n_fin<kDecR, kDecLW>, dim3(groups * 8 * a.nout), threads_n<8, kDecR, kDecLW>(), kDecLds,
+                     a, s);
+}
+
+}  // namespace lamd

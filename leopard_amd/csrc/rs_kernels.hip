@@ -236,8 +236,8 @@ LDEV auto prune16(const P& p) {
 // per-piece log-value table slots.
 template <int T, int R, int S>
 constexpr size_t lds16_dwords(int sets, int logs) {
-    return Tile16<T, R, S>::kXchDwords + size_t(sets) * (size_t(1) << T) * kTab16LdsDwords +
-           size_t(logs) * kTab16LdsDwords;
+    return Tile16<T, R, S>::kXchDwords + size_t(sets) * tab16_set_dwords(T) +
+           size_t(tab16_slot(logs));
 }
 
 // x[r] ^= the units of piece map pm at tile pieces piece(LAY, r, w), loaded in
@@ -298,7 +298,7 @@ __global__ void __launch_bounds__(threads16(T, R), LAMD_HI_WAVES) k_enc_hi(EncAr
     using TL = Tile16<T, R, S>;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t* iset = lds + TL::kXchDwords;
-    uint32_t* fset = iset + (size_t(1) << T) * kTab16LdsDwords;
+    uint32_t* fset = iset + tab16_set_dwords(T);
     const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const Cols16 cl = cols16(a.nunits, lane);
     const bool live = cl.live;
@@ -424,7 +424,7 @@ __global__ void __launch_bounds__(threads16(kLoBits, R), 4) k_dec_lo(DecArgs a) 
     using TL = Tile16<T, R, S>;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t* set = lds + TL::kXchDwords;
-    uint32_t* scl = set + (size_t(1) << T) * kTab16LdsDwords;
+    uint32_t* scl = set + tab16_set_dwords(T);
     const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const Cols16 cl = cols16(a.nunits, lane);
     const bool live = cl.live;
@@ -443,7 +443,7 @@ __global__ void __launch_bounds__(threads16(kLoBits, R), 4) k_dec_lo(DecArgs a) 
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) {
         asm volatile("" ::: "memory");  // keeps the compiler from hoisting every table read up here
-        const FF16::Tab t = FF16::tab_lds(scl + TL::piece(0, r, w) * kTab16LdsDwords);
+        const FF16::Tab t = FF16::tab_lds(scl + tab16_slot(TL::piece(0, r, w)));
 #pragma unroll
         for (int u = 0; u < C; ++u) FF16::mul(&v[r][u * 2], &v[r][u * 2], t);
 #pragma unroll
@@ -505,7 +505,7 @@ __global__ void __launch_bounds__(threads16(T, R), LAMD_HI_WAVES) k_dec_hi_half(
     using TL = Tile16<T, R, S>;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t* lset = lds + TL::kXchDwords;
-    uint32_t* hset = lset + (size_t(1) << T) * kTab16LdsDwords;
+    uint32_t* hset = lset + tab16_set_dwords(T);
     const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const Cols16 cl = cols16(a.nunits, lane);
     const bool live = cl.live;
@@ -544,7 +544,7 @@ __global__ void __launch_bounds__(threads16(kLoBits, R), 4) k_dec_fin(DecArgs a)
     // skip tiles holding no lost original (uniform across the workgroup)
     if (!((cload(a.needed_pyr + pyr_offset(T) + (y >> 5)) >> (y & 31)) & 1u)) return;
     uint32_t* set = lds + TL::kXchDwords;
-    uint32_t* rvl = set + (size_t(1) << T) * kTab16LdsDwords;
+    uint32_t* rvl = set + tab16_set_dwords(T);
     const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const Cols16 cl = cols16(a.nunits, lane);
     const bool live = cl.live;
@@ -572,7 +572,7 @@ __global__ void __launch_bounds__(threads16(kLoBits, R), 4) k_dec_fin(DecArgs a)
         if (p >= a.m && p < a.m + a.K && bit_set(a.erased_dev, p)) {
             uint32_t o[2 * C];
             asm volatile("" ::: "memory");
-            const FF16::Tab t = FF16::tab_lds(rvl + TL::piece(0, r, w) * kTab16LdsDwords);
+            const FF16::Tab t = FF16::tab_lds(rvl + tab16_slot(TL::piece(0, r, w)));
 #pragma unroll
             for (int u = 0; u < C; ++u) FF16::mul(&o[u * 2], &z[r][u * 2], t);
             st16(a.out.ptr(p - a.m) + cl.strip, cl.off, o);

@@ -4,4 +4,4 @@
 cd "$(dirname "$0")/.."
 d=leopard_amd/exp/$1; mkdir -p $d
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -fvisibility=hidden $2 -Iinclude -Ileopard_amd/csrc \
-   -shared -o $d/libleopard_amd.so leopard_amd/csrc/gf_tables.cpp leopard_amd/csrc/leopard_amd.cpp leopard_amd/csrc/rs_kernels.hip leopard_amd/csrc/rs_ff8.hip
+   -shared -o $d/libleopard_amd.so leopard_amd/csrc/*.cpp leopard_amd/csrc/*.hip

@@ -495,6 +495,28 @@ def configs4_sharded(args, leo, torch, device, barrier, rank, world, max_over_ra
     return res
 
 
+def kernels_for(k, r, nbytes, loss):
+    """The kernels the library runs for one encode / one decode of this shape
+    (mirrors the dispatch in leopard_amd.cpp; names as rocprofv3 lists them)."""
+    m = 1 << (r - 1).bit_length()
+    n = 1 << (m + k - 1).bit_length()
+    if n <= 256:
+        enc = "k_ff8_enc"
+        if loss == k == r == m:
+            dec = "k_ff8_enc (inverse form)"
+        elif 2 * m == n:
+            dec = "k_ff8_dec_half" if loss == k else "k_ff8_dec_split"
+        else:
+            dec = "k_ff8_dec"
+        return {"encode": enc, "decode": dec}
+    narrow = nbytes <= 256 << 10
+    enc = ("k_enc16n" if narrow and m in (128, 256) else
+           "k_enc_fused" if m <= 256 and not (m == 256 and k > m and nbytes < 512 << 10) else "k_enc_lo + k_enc_hi + k_enc_fin")
+    dec = ("k_dec16n_lo + k_dec16n_fin" if narrow and n <= 2048 else
+           "k_el16 (new pattern) + k_dec_lo + k_dec_hi%s + k_dec_fin" % ("_half" if loss == k and 2 * m == n else ""))
+    return {"encode": enc, "decode": dec}
+
+
 def run_shape(leo, torch, device, k, r, nbytes, loss, n=3):
     """One (K, R, B) shape: encode, then decode with `loss` originals lost (the
     benchmark's ShuffleDeck16 pattern, tests/benchmark.cpp:440-467).  Per-call
@@ -540,7 +562,7 @@ def run_shape(leo, torch, device, k, r, nbytes, loss, n=3):
     res = {"workload": f"{k}+{r} x {nbytes} B, {field}, {loss} originals lost", "encode_GBps": round(inb / te / 1e9, 3),
            "decode_GBps": round(inb / td / 1e9, 3), "encode_decode_GBps": round(inb / (te + td) / 1e9, 3),
            "encode_us": round(te * 1e6, 2), "decode_us": round(td * 1e6, 2), "roundtrip_ok": ok,
-           "buffer_sets": nsets,
+           "buffer_sets": nsets, "kernels": kernels_for(k, r, nbytes, loss),
            "roofline_frac": {"encode": round((k + r) * nbytes / te / 1e9 / HBM_PEAK_GBPS, 4),
                              "decode": round((k + loss) * nbytes / td / 1e9 / HBM_PEAK_GBPS, 4)}}
     del sets
@@ -601,12 +623,21 @@ def host_e2e_run(leo, k, r, nbytes, steps, register):
             "sample": f"{steps} steps of {k}+{r} x {nbytes} B encode + full-loss decode, {how}"}
 
 
+def _profile_order(path):
+    """(round, version) of profiles/rNN_vMM/...: newest first when sorted in reverse."""
+    import re
+    m = re.search(r"r(\d+)_v(\d+)", path)
+    return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
+
+
 def pmc_traffic(kernel, k, r, nbytes, objects=1):
-    """HBM bytes per launch of the dominant kernel from the committed PMC pass
-    (tools/pmc_traffic.py: FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md HBM
-    section), when one exists for this workload; else None."""
+    """HBM bytes per launch of the dominant kernel from the newest committed PMC
+    pass (tools/pmc_traffic.py: FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md
+    HBM section; profiles/rNN_vMM ordered by round, then version), when one
+    exists for this workload; else None."""
     import glob
-    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*", "pmc_traffic*.json")), reverse=True):
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*", "pmc_traffic*.json")), key=_profile_order,
+                       reverse=True):
         try:
             with open(path) as f:
                 d = json.load(f)

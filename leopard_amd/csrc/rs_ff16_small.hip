@@ -232,7 +232,7 @@ __global__ void __launch_bounds__((threads_n<8, R, LW>()), 4) k_dec16n_lo(DecArg
     if (!pyr_bit(a.present_pyr, T, y)) return;  // nothing received in this tile: U_y = 0, pass 2 skips it
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t* set = lds + TL::kXchDwords;
-    uint32_t* scl = set + tab16_set_dwords(T);
+    uint32_t* scl = lds;  // the scale tables share the exchange area: used before the first transpose
     const unsigned wave = uniform(threadIdx.x >> 6), lane = threadIdx.x & (LW - 1);
     const unsigned w = (wave << G) | ((threadIdx.x & 63u) >> (6 - G));
     const NarrowCols<LW> cl = narrow_cols<LW>(a.nunits, lane);
@@ -297,16 +297,12 @@ __global__ void __launch_bounds__((threads_n<8, R, LW>()), 4) k_dec16n_fin(DecAr
     if (!pyr_bit(a.needed_pyr, T, t)) return;  // no lost original in tile t
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t* fset = lds + TL::kXchDwords;
-    uint32_t* rvl = fset + tab16_set_dwords(T);
+    uint32_t* rvl = lds;  // the reveal tables go to the exchange area once the FFT is done with it
     const unsigned wave = uniform(threadIdx.x >> 6), lane = threadIdx.x & (LW - 1);
     const unsigned w = (wave << G) | ((threadIdx.x & 63u) >> (6 - G));
     const NarrowCols<LW> cl = narrow_cols<LW>(a.nunits, lane, strip);
     const uint32_t ew = a.erased_dev[(t << 3) + (w >> (5 - R))];  // layout 0: one word a lane
-    Tabs16Stage<NT, T> st;
-    LogTabs16Stage<NT, (1u << T)> ls;
-    st.load(a.sktab, -1, t << T, 0);
-    ls.load(a.tabs, a.reveal_logs + (t << T));
-    // U tile u (layout kLast: the layout the low IFFT ended in and the FFT starts in)
+    // U tile ut in layout kLast (the layout the low IFFT ended in and the FFT starts in)
     auto load_u = [&](typename TL::Reg& u, unsigned ut) {
 #pragma unroll
         for (int r = 0; r < TL::NR; ++r) {
@@ -314,17 +310,27 @@ __global__ void __launch_bounds__((threads_n<8, R, LW>()), 4) k_dec16n_fin(DecAr
             ld_unit(u[r], a.a_in.base + row * a.a_in.stride + a.a_in.off, cl.off);
         }
     };
-    st.store(fset);
-    ls.store(rvl);
-    __syncthreads();
-    typename TL::Reg z;
+    // the U tiles this output tile reads: received data and q[t ^ ut] != 0, or ut = t (D_lo)
+    auto wanted = [&](unsigned ut) {
+        return ut < a.nlo && pyr_bit(a.present_pyr, T, ut) && (ut == t || cload(a.qlog + (t ^ ut)) != kQZero);
+    };
+    {
+        Tabs16Stage<NT, T> st;
+        st.load(a.sktab, -1, t << T, 0);
+        st.store(fset);
+    }
+    typename TL::Reg z, u, nu;
     TL::zero(z);
-    for (unsigned ut = 0; ut < a.nlo; ++ut) {
-        if (!pyr_bit(a.present_pyr, T, ut)) continue;  // U = 0 (workgroup-uniform)
+    unsigned ut = 0;
+    while (ut < a.nlo && !wanted(ut)) ++ut;
+    if (ut < a.nlo) load_u(nu, ut);
+    __syncthreads();
+    while (ut < a.nlo) {
+        TL::copy(u, nu);
+        unsigned next = ut + 1;
+        while (next < a.nlo && !wanted(next)) ++next;
+        if (next < a.nlo) load_u(nu, next);  // in flight while this tile is folded in
         const uint32_t q = cload(a.qlog + (t ^ ut));
-        if (q == kQZero && ut != t) continue;
-        typename TL::Reg u;
-        load_u(u, ut);
         if (q == kQOne) {
             TL::xor_into(z, u);
         } else if (q != kQZero) {
@@ -338,12 +344,18 @@ __global__ void __launch_bounds__((threads_n<8, R, LW>()), 4) k_dec16n_fin(DecAr
         // the formal derivative's low bits: D_lo U_t (rs_device.h derivative_add)
         if (ut == t)
             TL::derivative_add(z, [&](int r, uint32_t* out) { out[0] = u[r][0]; out[1] = u[r][1]; }, w, lane, lds);
+        ut = next;
     }
+    LogTabs16Stage<NT, (1u << T)> ls;
+    ls.load(a.tabs, a.reveal_logs + (t << T));  // in flight during the FFT
     TL::fft(z, w, lane, lds, PieceSpace{0, 0, t << T}, LdsWindow16{fset, t << T, 0}, AllLive{});
+    __syncthreads();  // every wave is past the FFT's last exchange
+    ls.store(rvl);
     // lost original at p = m + i: work[i] = z[p] * exp(-el[p])  (LeopardFF16.cpp:1771-1773)
     auto pos = [&](int r) { return (t << T) + TL::piece(0, r, w); };
     uint64_t po[TL::NR];
     lane_ptrs(po, a.out, [&](int r) { return pos(r) >= a.m ? min(pos(r) - a.m, a.K - 1) : 0u; });
+    __syncthreads();
     if (!cl.live) return;
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) {
@@ -368,8 +380,9 @@ hipError_t launch16n(Kern* fn, dim3 grid, unsigned threads, size_t lds_bytes, co
 
 constexpr int kDecR = 3, kDecLW = 16;
 using DecTL = Tile<FF16, 8, kDecR, 1, kDecLW, 0, lg_bits(kDecLW)>;
-constexpr size_t kDecLds = (DecTL::kXchDwords + tab16_set_dwords(8) + tab16_slot(256)) * 4;
-static_assert(kDecLds <= 80 * 1024, "two workgroups per CU");
+constexpr size_t kDecLds = (DecTL::kXchDwords + tab16_set_dwords(8)) * 4;
+static_assert(kDecLds <= 160 * 1024 / 3, "three workgroups per CU");
+static_assert(tab16_slot(256) <= DecTL::kXchDwords, "log tables fit the exchange area");
 }  // namespace
 
 #ifdef LAMD_STAMPS

@@ -21,6 +21,8 @@
 #include <thread>
 #include <vector>
 
+#include <immintrin.h>
+
 #include "../../include/leopard.h"
 #include "../../include/leopard_amd.h"
 #include "gf_tables.h"
@@ -990,13 +992,43 @@ struct CopyJob {
     uint64_t len;
 };
 
-// memcpy of every job, split into <= 1 MiB parts spread over the pool.
+// Copy with non-temporal stores: the staging copies move every byte once and
+// neither side is read again soon, so streaming stores skip the read-for-
+// ownership of each destination line (a third of the memory traffic of a
+// cached copy) and leave the caches alone.  AVX2 when the CPU has it.
+__attribute__((target("avx2"))) void copy_stream_avx2(uint8_t* dst, const uint8_t* src, uint64_t n) {
+    const uint64_t head = std::min<uint64_t>(n, (32 - (reinterpret_cast<uintptr_t>(dst) & 31)) & 31);
+    std::memcpy(dst, src, head);
+    dst += head;
+    src += head;
+    n -= head;
+    uint64_t i = 0;
+    for (; i + 128 <= n; i += 128) {
+        const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i));
+        const __m256i b = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i + 32));
+        const __m256i c = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i + 64));
+        const __m256i d = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i + 96));
+        _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i), a);
+        _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i + 32), b);
+        _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i + 64), c);
+        _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i + 96), d);
+    }
+    std::memcpy(dst + i, src + i, n - i);
+    _mm_sfence();  // the streamed lines are visible before the copy engine or the caller reads them
+}
+void copy_stream(uint8_t* dst, const uint8_t* src, uint64_t n) {
+    static const bool avx2 = __builtin_cpu_supports("avx2");
+    if (avx2 && n >= 4096) copy_stream_avx2(dst, src, n);
+    else std::memcpy(dst, src, n);
+}
+
+// Copy of every job, split into <= 1 MiB parts spread over the pool.
 void parallel_copy(const std::vector<CopyJob>& jobs) {
     constexpr uint64_t kPart = 1 << 20;
     std::vector<CopyJob> parts;
     for (const CopyJob& j : jobs)
         for (uint64_t o = 0; o < j.len; o += kPart) parts.push_back({j.dst + o, j.src + o, std::min(kPart, j.len - o)});
-    CpuPool::get().run(unsigned(parts.size()), [&](unsigned i) { std::memcpy(parts[i].dst, parts[i].src, parts[i].len); });
+    CpuPool::get().run(unsigned(parts.size()), [&](unsigned i) { copy_stream(parts[i].dst, parts[i].src, parts[i].len); });
 }
 
 // Device work for one slice: inputs are rows [0, nin) of `din`, outputs rows

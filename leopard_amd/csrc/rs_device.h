@@ -49,6 +49,12 @@
 
 namespace lamd {
 
+// Native clang vectors, not HIP's uint4/uint2: those are unions wrapped in a
+// struct, and a local array of them is not promoted to registers (it lives in
+// scratch memory, stored and reloaded around every asm barrier).
+using v4u = unsigned __attribute__((ext_vector_type(4)));
+using v2u = unsigned __attribute__((ext_vector_type(2)));
+
 LDEV uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) { return __builtin_amdgcn_perm(hi, lo, sel); }
 LDEV uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
 LDEV unsigned uniform(unsigned v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -96,7 +102,7 @@ struct FF8 {
     }
     LDEV static Tab tab(const uint32_t* tabs, unsigned log_m) { return tab_at(tabs + log_m * kTabDw); }
     LDEV static Tab tab_lds(const uint32_t* p) {
-        const uint4 v = *reinterpret_cast<const uint4*>(p);
+        const v4u v = *reinterpret_cast<const v4u*>(p);
         return Tab{v.x, v.y, v.z, v.w, p[4]};
     }
     LDEV static uint32_t prod(uint32_t y, const Tab& t) {
@@ -136,7 +142,7 @@ struct FF16 {
         Tab r;
 #pragma unroll
         for (int i = 0; i < 5; ++i) {
-            const uint4 v = reinterpret_cast<const uint4*>(p)[i];
+            const v4u v = reinterpret_cast<const v4u*>(p)[i];
             r.t[4 * i] = v.x;
             r.t[4 * i + 1] = v.y;
             r.t[4 * i + 2] = v.z;
@@ -213,9 +219,9 @@ struct VecT;
 template <>
 struct VecT<1> { using type = uint32_t; };
 template <>
-struct VecT<2> { using type = uint2; };
+struct VecT<2> { using type = v2u; };
 template <>
-struct VecT<4> { using type = uint4; };
+struct VecT<4> { using type = v4u; };
 
 template <int C>
 LDEV void vload(uint32_t* dst, const uint8_t* src) {
@@ -296,7 +302,7 @@ struct LdsTab8 {
     uint32_t* base;
     static constexpr size_t kDwords = 5 * size_t(N);
     LDEV FF8::Tab at(int i) const {
-        const uint4 v = reinterpret_cast<const uint4*>(base)[i];
+        const v4u v = reinterpret_cast<const v4u*>(base)[i];
         return FF8::Tab{v.x, v.y, v.z, v.w, base[4 * N + i]};
     }
 };
@@ -364,9 +370,9 @@ constexpr size_t kTab16LdsDwords = 20;
 // the piece loads), store() writes LDS after the piece loads are in flight.
 template <int NT, int T>
 struct Tabs16Stage {
-    static constexpr unsigned kVec = ((1u << T) - 1) * 5;  // uint4 per set (slot 0 unused)
+    static constexpr unsigned kVec = ((1u << T) - 1) * 5;  // v4u per set (slot 0 unused)
     static constexpr unsigned PER = (kVec + NT - 1) / NT;
-    uint4 v[PER];
+    v4u v[PER];
     LDEV void load(const uint32_t* sktab, int base, unsigned hi_fixed, unsigned l0) {
         static_for<0, int(PER)>([&](auto I) __attribute__((always_inline)) {
             constexpr unsigned i = decltype(I)::value;
@@ -374,7 +380,7 @@ struct Tabs16Stage {
             if constexpr ((i + 1) * NT > kVec) e = e < kVec ? e : kVec - 1;
             const unsigned j = 1 + e / 5, k = e % 5;
             const size_t entry = size_t(int64_t(base) + int64_t(hi_fixed + (j << l0)));
-            v[i] = reinterpret_cast<const uint4*>(sktab)[entry * 6 + k];  // 24-dword entries
+            v[i] = reinterpret_cast<const v4u*>(sktab)[entry * 6 + k];  // 24-dword entries
         });
     }
     LDEV void store(uint32_t* set) const {
@@ -382,7 +388,7 @@ struct Tabs16Stage {
             constexpr unsigned i = decltype(I)::value;
             const unsigned e = threadIdx.x + i * NT;
             const unsigned j = 1 + e / 5, k = e % 5;
-            if ((i + 1) * NT <= kVec || e < kVec) reinterpret_cast<uint4*>(set)[tab16_slot(j) / 4 + k] = v[i];
+            if ((i + 1) * NT <= kVec || e < kVec) reinterpret_cast<v4u*>(set)[tab16_slot(j) / 4 + k] = v[i];
         });
     }
 };
@@ -394,14 +400,14 @@ template <int NT, unsigned N>
 struct LogTabs16Stage {
     static constexpr unsigned kVec = N * 5;
     static constexpr unsigned PER = (kVec + NT - 1) / NT;
-    uint4 v[PER];
+    v4u v[PER];
     LDEV void load(const uint32_t* tabs, const uint32_t* logs) {
         static_for<0, int(PER)>([&](auto I) __attribute__((always_inline)) {
             constexpr unsigned i = decltype(I)::value;
             unsigned e = threadIdx.x + i * NT;
             if constexpr ((i + 1) * NT > kVec) e = e < kVec ? e : kVec - 1;
             const unsigned lm = logs[e / 5];
-            v[i] = reinterpret_cast<const uint4*>(tabs)[size_t(lm) * 6 + e % 5];
+            v[i] = reinterpret_cast<const v4u*>(tabs)[size_t(lm) * 6 + e % 5];
         });
     }
     // slot p (the table of logs[p]) at dword tab16_slot(p), as the skew sets
@@ -409,7 +415,7 @@ struct LogTabs16Stage {
         static_for<0, int(PER)>([&](auto I) __attribute__((always_inline)) {
             constexpr unsigned i = decltype(I)::value;
             const unsigned e = threadIdx.x + i * NT;
-            if ((i + 1) * NT <= kVec || e < kVec) reinterpret_cast<uint4*>(dst)[tab16_slot(e / 5) / 4 + e % 5] = v[i];
+            if ((i + 1) * NT <= kVec || e < kVec) reinterpret_cast<v4u*>(dst)[tab16_slot(e / 5) / 4 + e % 5] = v[i];
         });
     }
 };
@@ -421,7 +427,7 @@ struct LogTabs16Stage {
 template <int NT, unsigned N>
 struct TabStage8 {
     static constexpr unsigned PER = (N + NT - 1) / NT;  // entries per thread
-    uint4 va[PER];
+    v4u va[PER];
     uint32_t vc[PER];
     LDEV void load(const uint32_t* src) {
         if constexpr ((LAMD_ABLATE & 256) != 0) return;
@@ -429,7 +435,7 @@ struct TabStage8 {
             constexpr unsigned i = decltype(I)::value;
             unsigned e = threadIdx.x + i * NT;
             if constexpr ((i + 1) * NT > N) e = e < N ? e : N - 1;  // tail: re-read a valid entry
-            va[i] = reinterpret_cast<const uint4*>(src)[2 * e];
+            va[i] = reinterpret_cast<const v4u*>(src)[2 * e];
             vc[i] = src[8 * e + 4];
         });
     }
@@ -441,7 +447,7 @@ struct TabStage8 {
             constexpr unsigned i = decltype(I)::value;
             const unsigned e = threadIdx.x + i * NT;
             if ((i + 1) * NT <= N || e < N) {
-                reinterpret_cast<uint4*>(dst.base)[e] = va[i];
+                reinterpret_cast<v4u*>(dst.base)[e] = va[i];
                 dst.base[4 * M + e] = vc[i];
             }
         });

@@ -652,13 +652,13 @@ __global__ void __launch_bounds__(64) k_el16_cols(uint32_t* tmp, const uint32_t*
 __global__ void __launch_bounds__(256) k_xor_reduce(XorArgs a) {
     const uint64_t q = (uint64_t(blockIdx.x) * 256 + threadIdx.x) * 4;  // dword index
     if (q >= a.ndwords) return;
-    uint4 acc = make_uint4(0, 0, 0, 0);
+    v4u acc = v4u{0, 0, 0, 0};
     for (unsigned i = 0; i < a.count; ++i) {
         const uint8_t* p = a.src.ptr(i);
-        const uint4 v = *gptr<const uint4>(p + q * 4);
+        const v4u v = *gptr<const v4u>(p + q * 4);
         acc.x ^= v.x; acc.y ^= v.y; acc.z ^= v.z; acc.w ^= v.w;
     }
-    *gptr<uint4>(a.out.ptr(0) + q * 4) = acc;
+    *gptr<v4u>(a.out.ptr(0) + q * 4) = acc;
 }
 
 // ------------------------------------------------------------ dispatching --

@@ -42,6 +42,12 @@ __device__ uint64_t* g_stamps;
     do {         \
     } while (0)
 #endif
+#ifdef LAMD_CLOCK
+// Diagnostic builds only (tools/clock.py): per workgroup of the slab batch
+// kernel, (s_memtime, s_memrealtime) at entry and exit of wave 0, for the
+// in-kernel shader clock (MI355X_MICROARCH.md "DVFS give-back" item 6).
+__device__ uint64_t* g_clock;
+#endif
 
 namespace {
 
@@ -375,7 +381,17 @@ __global__ void __launch_bounds__(threads_for(T, RB), 4) k_ff8_enc_batch(const F
 #endif
 template <int T, int RB, bool kMulti, int kForm = kFormGeneral>
 __global__ void __launch_bounds__(threads_for(T, RB), LAMD_SLAB_WAVES) k_ff8_enc_slab(Ff8SlabBatch b) {
+#ifdef LAMD_CLOCK
+    const uint64_t c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+#endif
     ff8_enc<T, RB, kMulti, 1, 0, kForm>(Ff8SlabView(b, blockIdx.y));
+#ifdef LAMD_CLOCK
+    const uint64_t c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) {
+        uint64_t* o = g_clock + 4ull * (blockIdx.x + uint64_t(blockIdx.y) * gridDim.x);
+        o[0] = c0; o[1] = r0; o[2] = c1; o[3] = r1;
+    }
+#endif
 }
 
 // --------------------------------------------------------------- decode -----
@@ -835,6 +851,11 @@ hipError_t dec_split_T(const Ff8DecArgs& a, hipStream_t s) {
 
 }  // namespace
 
+#ifdef LAMD_CLOCK
+extern "C" __attribute__((visibility("default"))) int leo_amd_debug_clock(void* buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_clock), &buf, sizeof(buf)) == hipSuccess ? 0 : -1;
+}
+#endif
 #ifdef LAMD_STAMPS
 extern "C" __attribute__((visibility("default"))) int leo_amd_debug_stamps(void* buf) {
     return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &buf, sizeof(buf)) == hipSuccess ? 0 : -1;

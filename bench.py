@@ -617,7 +617,7 @@ def host_e2e_run(leo, k, r, nbytes, steps, register):
             leo.unregister_host(arr.ctypes.data)
     inb = k * nbytes
     how = ("registered host buffers (leo_amd_register_host): kernels read and write them in place over PCIe"
-           if register else "pageable numpy buffers: pinned staging ring, H2D + kernels + D2H per call")
+           if register else "pageable numpy buffers (rows of one array): direct SDMA row copies H2D, kernels, D2H per call")
     return {"value": round(inb * steps / dt / 1e9, 3), "unit": "GB/s", "encode_GBps": round(inb * steps / t_enc / 1e9, 3),
             "decode_GBps": round(inb * steps / (dt - t_enc) / 1e9, 3), "roundtrip_ok": ok,
             "sample": f"{steps} steps of {k}+{r} x {nbytes} B encode + full-loss decode, {how}"}

@@ -216,6 +216,9 @@ struct Workspace {
     // error-locator launches.
     uint8_t* dec16 = nullptr;
     std::vector<uint32_t> dec16_key;
+    // Device rows of a host call staged by direct SDMA copies (run_host_direct).
+    uint8_t* direct = nullptr;
+    size_t direct_size = 0;
 
     ~Workspace() { release(); }
     // Waits for the work that may still use this workspace, then frees it.
@@ -231,7 +234,7 @@ struct Workspace {
             if (sl.done) (void)hipEventDestroy(sl.done);
             sl = StageSlot{};
         }
-        release_device_memory(dev, {dbuf, dec16, ring_dev});
+        release_device_memory(dev, {dbuf, dec16, ring_dev, direct});
         if (ring_host) (void)hipHostFree(ring_host);
         for (int s = 0; s < 2; ++s) {
             if (pipe_stream[s]) (void)hipStreamDestroy(pipe_stream[s]);
@@ -241,9 +244,9 @@ struct Workspace {
             in_done[s] = out_done[s] = nullptr;
         }
         if (last_use) (void)hipEventDestroy(last_use);
-        dbuf = dec16 = ring_dev = ring_host = ring_host_dev = nullptr;
+        dbuf = dec16 = ring_dev = ring_host = ring_host_dev = direct = nullptr;
         last_use = nullptr;
-        dsize = slot_bytes = 0;
+        dsize = slot_bytes = direct_size = 0;
     }
     // Called at the end of every call: marks where the work of this call that
     // uses the workspace's memory ends on the stream.
@@ -291,6 +294,17 @@ struct Workspace {
         dsize = 0;
         HIP_OK(hipMallocAsync(reinterpret_cast<void**>(&dbuf), want, stream), "allocate scratch");
         dsize = want;
+        return Leopard_Success;
+    }
+    // Device rows for run_host_direct, stream-ordered like the arena.
+    LeopardResult reserve_direct(size_t bytes) {
+        touched = true;
+        if (bytes <= direct_size) return Leopard_Success;
+        if (direct) HIP_OK(hipFreeAsync(direct, stream), "free direct rows");
+        direct = nullptr;
+        direct_size = 0;
+        HIP_OK(hipMallocAsync(reinterpret_cast<void**>(&direct), bytes, stream), "allocate direct rows");
+        direct_size = bytes;
         return Leopard_Success;
     }
     // Copies `bytes` from host memory src (or, with src == nullptr, lets
@@ -1066,17 +1080,90 @@ int pipe_mode() {
 #endif
 }
 
+// Pieces that follow each other at one stride (rows of one caller array): a
+// run is one copy (1-D when the stride is the piece length, else 2-D).
+struct HostRun {
+    uint64_t first, count, stride;
+};
+template <class P>
+std::vector<HostRun> host_runs(const std::vector<P>& v, uint64_t bytes) {
+    std::vector<HostRun> runs;
+    for (uint64_t i = 0; i < v.size(); ++i) {
+        if (!runs.empty()) {
+            HostRun& b = runs.back();
+            const uint8_t* prev = v[i - 1];
+            const uint8_t* cur = v[i];
+            if (cur > prev) {
+                const uint64_t d = uint64_t(cur - prev);
+                if (d >= bytes && (b.count == 1 ? true : d == b.stride)) {
+                    b.stride = d;
+                    ++b.count;
+                    continue;
+                }
+            }
+        }
+        runs.push_back({i, 1, bytes});
+    }
+    return runs;
+}
+constexpr size_t kDirectMaxRuns = 16;                 // more runs: the gather / scatter ring
+constexpr uint64_t kDirectMaxBytes = 8ull << 30;      // device rows of one direct call
+
+// Host pieces that form a few row runs (the usual caller layout: pieces are
+// rows of one or a few arrays) go straight between the caller's pageable
+// memory and device rows by SDMA, one copy per run: no host copies at all.
+// The copy engines read and write pageable memory at the PCIe rate (53 GB/s
+// each way, profiles/r03_v2/hostcopy.txt), where the gather / scatter ring is
+// bound by host memcpy.  Returns Leopard_Success with *done = false when the
+// layout does not qualify.
+LeopardResult run_host_direct(Call& c, uint64_t bytes, const std::vector<const uint8_t*>& hin,
+                              const std::vector<uint8_t*>& hout, const SliceFn& fn, bool* done) {
+    *done = false;
+    const uint64_t nin = hin.size(), nout = hout.size(), rows = nin + nout;
+    if (rows * bytes > kDirectMaxBytes) return Leopard_Success;
+    const std::vector<HostRun> rin = host_runs(hin, bytes), rout = host_runs(hout, bytes);
+    if (rin.size() + rout.size() > kDirectMaxRuns) return Leopard_Success;
+    Workspace& ws = *c.ws;
+    LeopardResult r = ws.reserve_direct(rows * bytes);
+    if (r != Leopard_Success) return r;
+    uint8_t* din = ws.direct;
+    uint8_t* dout = ws.direct + nin * bytes;
+    for (const HostRun& run : rin) {
+        uint8_t* dst = din + run.first * bytes;
+        if (run.stride == bytes)
+            HIP_OK(hipMemcpyAsync(dst, hin[run.first], run.count * bytes, hipMemcpyHostToDevice, c.s), "upload rows");
+        else
+            HIP_OK(hipMemcpy2DAsync(dst, bytes, hin[run.first], run.stride, bytes, run.count, hipMemcpyHostToDevice, c.s),
+                   "upload rows");
+    }
+    if ((r = fn(c, bytes, din, dout, bytes)) != Leopard_Success) return r;
+    HIP_OK(hipGetLastError(), "kernel launch");
+    for (const HostRun& run : rout) {
+        const uint8_t* src = dout + run.first * bytes;
+        if (run.stride == bytes)
+            HIP_OK(hipMemcpyAsync(hout[run.first], src, run.count * bytes, hipMemcpyDeviceToHost, c.s), "download rows");
+        else
+            HIP_OK(hipMemcpy2DAsync(hout[run.first], run.stride, src, bytes, bytes, run.count, hipMemcpyDeviceToHost, c.s),
+                   "download rows");
+    }
+    *done = true;
+    return Leopard_Success;
+}
+
 // hin: host input pieces (call offset applied); hout: host output pieces.
 // Slot j & 1 runs on its own stream with its own scratch (per-stream workspaces).
 LeopardResult run_host_pipeline(Call& c, uint64_t bytes, const std::vector<const uint8_t*>& hin,
                                 const std::vector<uint8_t*>& hout, const SliceFn& fn) {
+    bool direct = false;
+    LeopardResult r = run_host_direct(c, bytes, hin, hout, fn, &direct);
+    if (r != Leopard_Success || direct) return r;
     const uint64_t nin = hin.size(), nout = hout.size(), rows = nin + nout;
     uint64_t slice = bytes;
     if (rows * bytes > pipe_slot_budget())  // >= 4 KiB slices even when that outgrows the budget
         slice = std::max<uint64_t>(pipe_slot_budget() / rows / 64 * 64, std::min<uint64_t>(bytes, 4096));
     if (rows * bytes > (4ull << 20)) slice = std::min<uint64_t>(slice, (bytes / 4 + 63) / 64 * 64);  // >= 4 slices
     const uint64_t in_bytes = nin * slice, slot = rows * slice;
-    LeopardResult r = c.ws->reserve_ring(slot);
+    r = c.ws->reserve_ring(slot);
     if (r != Leopard_Success) return r;
     Workspace& ws = *c.ws;
     const unsigned nslices = unsigned((bytes + slice - 1) / slice);

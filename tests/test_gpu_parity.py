@@ -394,6 +394,53 @@ def test_host_pipeline_roundtrip(leo, k, r, b, loss):
         assert np.array_equal(dwork[i], data[i]), i
 
 
+@pytest.mark.parametrize("k,r,b,layout", [(128, 128, 1 << 16, "strided"), (128, 128, 1 << 16, "scattered"),
+                                          (1000, 200, 4096, "strided"), (1000, 200, 4096, "scattered"),
+                                          (200, 55, 64 * 100, "two_arrays")])
+def test_host_layouts_direct_and_ring(leo, k, r, b, layout):
+    """The two host-memory paths: pieces forming a few row runs go by direct
+    SDMA copies (1-D for dense rows, 2-D for rows of a wider array:
+    "strided", "two_arrays"), pieces at scattered addresses through the
+    gather / scatter ring ("scattered": one allocation per piece, handed over
+    in descending address order, so no two form a run).  Encode must match the
+    oracle and the decode of every lost original must rebuild it."""
+    data = ol.pcg_bytes(8, k, k, b)
+    wc, dwc = leo.leo_encode_work_count(k, r), leo.leo_decode_work_count(k, r)
+
+    def rows(n, fill=None):
+        if layout == "strided":  # rows of a wider array: stride b + 192
+            big = np.zeros((n, b + 192), dtype=np.uint8)
+            v = [big[i, 64:64 + b] for i in range(n)]
+        elif layout == "two_arrays":
+            h = n // 2
+            a1, a2 = np.zeros((h, b), dtype=np.uint8), np.zeros((n - h, b), dtype=np.uint8)
+            v = [a1[i] for i in range(h)] + [a2[i] for i in range(n - h)]
+        else:
+            v = [np.zeros(b, dtype=np.uint8) for _ in range(n)]
+            v.sort(key=lambda x: -x.ctypes.data)  # descending addresses: never a run
+        if fill is not None:
+            for i in range(n):
+                v[i][:] = fill[i]
+        return v
+
+    din = rows(k, data)
+    work = rows(wc)
+    res = leo.leo_encode(b, k, r, wc, [x.ctypes.data for x in din], [x.ctypes.data for x in work])
+    assert res == leo.LeopardResult.Success, leo.last_error()
+    rec = np.stack(work[:r])
+    assert np.array_equal(rec, ol.oracle().encode(data, r))
+    loss = min(k, r)
+    lo, lr = ol.benchmark_losses(k, r, loss, seed=8, trial=k)
+    recv = rows(r, rec)
+    dwork = rows(dwc)
+    res = leo.leo_decode(b, k, r, dwc, [None if i in lo else din[i].ctypes.data for i in range(k)],
+                         [None if i in lr else recv[i].ctypes.data for i in range(r)],
+                         [x.ctypes.data for x in dwork])
+    assert res == leo.LeopardResult.Success, leo.last_error()
+    for i in lo:
+        assert np.array_equal(dwork[i], data[i]), i
+
+
 def test_host_edge_paths(leo):
     """K == 1 and zero-loss host calls are copies (leopard.cpp:143-149, 279-291)."""
     d = ol.pcg_bytes(6, 0, 1, 640)

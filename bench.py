@@ -6,15 +6,21 @@ Metric (BASELINE.json): device-resident encode+decode GB/s of input bytes
 tests/benchmark.cpp:521-524).
 
 Headline workload (configs[1]): 128 originals + 128 recovery pieces of 65536
-bytes, GF(2^8).  One *step* = one pass over a batch of OBJECTS independent
-objects (default 16, a storage node's stripes): each is encoded and then
-decoded with every original lost (the benchmark's worst case, rebuilt from the
-128 recovery pieces), all through the drop-in C ABI with device pointers in
-async mode; object o of a step runs on HIP stream o % S (S objects in flight,
---streams).  The batch cycles through >= 16 distinct buffer sets (> 2x the
-256 MiB Infinity Cache), so every step reads HBM.  Every rank codes its own
-objects (64-byte column blocks and objects never interact; no collective):
-"scaling": "weak", value = input bytes of all ranks / max-over-ranks time.
+bytes, GF(2^8).  One *step* = one pass over OBJECTS independent objects
+(default 64, a storage node's stripes): each is encoded and then decoded with
+every original lost (the benchmark's worst case, rebuilt from the 128 recovery
+pieces).  Default mode "batch": the objects go out in launches of
+--launch-objects (default 16) through the leo_amd_encode_batch /
+leo_amd_decode_batch extension (one kernel per 16 objects), consecutive launch
+pairs alternating over 2 streams; the line records mode and objects per launch.
+`modes` also carries the drop-in comparable figures through the reference
+C ABI: "calls_in_flight" (leo_encode + leo_decode per object, 3 streams in
+flight, async device pointers) and "serial" (one stream, each call waiting for
+the previous: a plain drop-in caller).  The steps cycle through enough buffer
+sets to exceed 512 MiB (> 2x the 256 MiB Infinity Cache), so every step reads
+HBM.  Every rank codes its own objects (64-byte column blocks and objects never
+interact; no collective): "scaling": "weak", value = input bytes of all ranks /
+max-over-ranks time.
 
 configs[4] (`sharded_object`): ONE 32768+32768 x 64 KiB object (2 GiB of
 originals, GF(2^16)) column-sharded over the N ranks -- rank g runs

@@ -175,6 +175,23 @@ struct FF16 {
                     xor3(perm(t[15], t[14], b1), perm(t[17], t[17], a2), perm(t[19], t[19], b2)));
     }
     LDEV static void mul(uint32_t* x, const uint32_t* y, const Tab& t) { prod(y[0], y[1], t, x[0], x[1]); }
+    // The six perm selectors of y, for several multiplies of the same y.
+    struct Sel {
+        uint32_t a0, a1, a2, b0, b1, b2;
+    };
+    LDEV static Sel sel(const uint32_t* y) {
+        const uint32_t lo = y[0], hi = y[1];
+        return Sel{lo & 0x07070707u, (lo >> 3) & 0x07070707u, (lo >> 6) & 0x03030303u,
+                   hi & 0x07070707u, (hi >> 3) & 0x07070707u, (hi >> 6) & 0x03030303u};
+    }
+    // x ^= y * c with y's selectors s
+    LDEV static void muladd_sel(uint32_t* x, const Sel& s, const Tab& T) {
+        const uint32_t* t = T.t;
+        x[0] = xor3(x[0], xor3(perm(t[1], t[0], s.a0), perm(t[5], t[4], s.a1), perm(t[9], t[8], s.b0)),
+                    xor3(perm(t[13], t[12], s.b1), perm(t[16], t[16], s.a2), perm(t[18], t[18], s.b2)));
+        x[1] = xor3(x[1], xor3(perm(t[3], t[2], s.a0), perm(t[7], t[6], s.a1), perm(t[11], t[10], s.b0)),
+                    xor3(perm(t[15], t[14], s.b1), perm(t[17], t[17], s.a2), perm(t[19], t[19], s.b2)));
+    }
 };
 
 // ------------------------------------------------------------ piece maps ---
@@ -374,6 +391,7 @@ struct Tabs16Stage {
     static constexpr unsigned PER = (kVec + NT - 1) / NT;
     v4u v[PER];
     LDEV void load(const uint32_t* sktab, int base, unsigned hi_fixed, unsigned l0) {
+        if constexpr ((LAMD_ABLATE & 256) != 0) return;
         static_for<0, int(PER)>([&](auto I) __attribute__((always_inline)) {
             constexpr unsigned i = decltype(I)::value;
             unsigned e = threadIdx.x + i * NT;
@@ -384,6 +402,7 @@ struct Tabs16Stage {
         });
     }
     LDEV void store(uint32_t* set) const {
+        if constexpr ((LAMD_ABLATE & 256) != 0) return;
         static_for<0, int(PER)>([&](auto I) __attribute__((always_inline)) {
             constexpr unsigned i = decltype(I)::value;
             const unsigned e = threadIdx.x + i * NT;
@@ -402,6 +421,7 @@ struct LogTabs16Stage {
     static constexpr unsigned PER = (kVec + NT - 1) / NT;
     v4u v[PER];
     LDEV void load(const uint32_t* tabs, const uint32_t* logs) {
+        if constexpr ((LAMD_ABLATE & 256) != 0) return;
         static_for<0, int(PER)>([&](auto I) __attribute__((always_inline)) {
             constexpr unsigned i = decltype(I)::value;
             unsigned e = threadIdx.x + i * NT;
@@ -412,6 +432,7 @@ struct LogTabs16Stage {
     }
     // slot p (the table of logs[p]) at dword tab16_slot(p), as the skew sets
     LDEV void store(uint32_t* dst) const {
+        if constexpr ((LAMD_ABLATE & 256) != 0) return;
         static_for<0, int(PER)>([&](auto I) __attribute__((always_inline)) {
             constexpr unsigned i = decltype(I)::value;
             const unsigned e = threadIdx.x + i * NT;

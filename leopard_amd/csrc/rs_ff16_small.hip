@@ -290,27 +290,49 @@ __global__ void __launch_bounds__((threads_n<8, R, LW>()), 4) k_dec16n_lo(DecArg
     }
 }
 
-template <int R, int LW>
-__global__ void __launch_bounds__((threads_n<8, R, LW>()), 4) k_dec16n_fin(DecArgs a) {
+// Pass 2 over NZ consecutive output tiles per workgroup: every U tile is read
+// once for all of them and its perm selectors are formed once for all of their
+// multiplies.  NZ = 2 measured slower than 1 (its registers allow one
+// workgroup per CU instead of two: 1000+200 x 64 KiB decode 203 vs 181 us,
+// profiles/r03_v4/dec_nz_ab.txt), so the default is 1.  Prefetching U two
+// tiles ahead instead of one measured equal (179 vs 180 us) and was dropped.
+#ifndef LAMD_DEC16N_NZ  // output tiles per pass-2 workgroup (2 measured slower: occupancy, r03_v4)
+#define LAMD_DEC16N_NZ 1
+#endif
+#ifndef LAMD_DEC16N_FIN_WAVES  // waves per SIMD the pass-2 register budget is cut for
+#define LAMD_DEC16N_FIN_WAVES (LAMD_DEC16N_NZ > 1 ? 3 : 4)
+#endif
+template <int R, int LW, int NZ>
+__global__ void __launch_bounds__((threads_n<8, R, LW>()), LAMD_DEC16N_FIN_WAVES) k_dec16n_fin(DecArgs a) {
     if constexpr ((LAMD_ABLATE & 16) != 0) return;
     constexpr int T = 8, G = lg_bits(LW);
     using TL = Tile<FF16, T, R, 1, LW, 0, G>;
     constexpr unsigned NT = threads_n<T, R, LW>();
-    // workgroup i runs on XCD i % 8: the nout workgroups of one strip (its
+    constexpr size_t kSet = tab16_set_dwords(T);
+    // workgroup i runs on XCD i % 8: the workgroups of one strip (its groups of
     // output tiles) are dealt to one XCD back to back, so the U tiles they all
     // read come from that XCD's L2
+    const unsigned ngrp = (a.nout + NZ - 1) / NZ;
     const unsigned j = blockIdx.x >> 3;
-    const uint64_t strip = (blockIdx.x & 7u) + 8ull * (j / a.nout);
-    const unsigned t = a.tile0 + j % a.nout;
+    const uint64_t strip = (blockIdx.x & 7u) + 8ull * (j / ngrp);
     if (strip * LW >= a.nunits) return;
-    if (!pyr_bit(a.needed_pyr, T, t)) return;  // no lost original in tile t
+    unsigned t[NZ];
+    bool live[NZ];
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < NZ; ++k) {
+        t[k] = a.tile0 + (j % ngrp) * NZ + k;
+        live[k] = t[k] < a.tile0 + a.nout && pyr_bit(a.needed_pyr, T, t[k]);  // tile holds a lost original
+        any |= live[k];
+    }
+    if (!any) return;
+    STAMP16(0);
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    uint32_t* fset = lds + TL::kXchDwords;
-    uint32_t* rvl = lds;  // the reveal tables go to the exchange area once the FFT is done with it
+    uint32_t* rvl = lds;  // the reveal tables go to the exchange area once an FFT is done with it
+    auto fset = [&](int k) { return lds + TL::kXchDwords + size_t(k) * kSet; };
     const unsigned wave = uniform(threadIdx.x >> 6), lane = threadIdx.x & (LW - 1);
     const unsigned w = (wave << G) | ((threadIdx.x & 63u) >> (6 - G));
     const NarrowCols<LW> cl = narrow_cols<LW>(a.nunits, lane, strip);
-    const uint32_t ew = a.erased_dev[(t << 3) + (w >> (5 - R))];  // layout 0: one word a lane
     // U tile ut in layout kLast (the layout the low IFFT ended in and the FFT starts in)
     auto load_u = [&](typename TL::Reg& u, unsigned ut) {
 #pragma unroll
@@ -319,63 +341,102 @@ __global__ void __launch_bounds__((threads_n<8, R, LW>()), 4) k_dec16n_fin(DecAr
             ld_unit(u[r], a.a_in.base + row * a.a_in.stride + a.a_in.off, cl.off);
         }
     };
-    // the U tiles this output tile reads: received data and q[t ^ ut] != 0, or ut = t (D_lo)
+    // the U tiles read: received data, and q[t ^ ut] != 0 or ut = t (D_lo) for a live output t
     auto wanted = [&](unsigned ut) {
-        return ut < a.nlo && pyr_bit(a.present_pyr, T, ut) && (ut == t || cload(a.qlog + (t ^ ut)) != kQZero);
+        if (!(ut < a.nlo && pyr_bit(a.present_pyr, T, ut))) return false;
+        bool want = false;
+#pragma unroll
+        for (int k = 0; k < NZ; ++k) want |= live[k] && (ut == t[k] || cload(a.qlog + (t[k] ^ ut)) != kQZero);
+        return want;
     };
-    {
-        Tabs16Stage<NT, T> st;
-        st.load(a.sktab, -1, t << T, 0);
-        st.store(fset);
-    }
-    typename TL::Reg z, u, nu;
-    TL::zero(z);
+#pragma unroll
+    for (int k = 0; k < NZ; ++k)
+        if (live[k]) {
+            Tabs16Stage<NT, T> st;
+            st.load(a.sktab, -1, t[k] << T, 0);
+            st.store(fset(k));
+        }
+    typename TL::Reg z[NZ], u, nu;
+#pragma unroll
+    for (int k = 0; k < NZ; ++k) TL::zero(z[k]);
     unsigned ut = 0;
     while (ut < a.nlo && !wanted(ut)) ++ut;
     if (ut < a.nlo) load_u(nu, ut);
     __syncthreads();
+    STAMP16(1);
     while (ut < a.nlo) {
         TL::copy(u, nu);
         unsigned next = ut + 1;
         while (next < a.nlo && !wanted(next)) ++next;
         if (next < a.nlo) load_u(nu, next);  // in flight while this tile is folded in
-        const uint32_t q = cload(a.qlog + (t ^ ut));
-        if (q == kQOne) {
-            TL::xor_into(z, u);
-        } else if (q != kQZero) {
-            const FF16::Tab tq = FF16::tab(a.tabs, q);
+        uint32_t q[NZ];
+        unsigned mulmask = 0;
 #pragma unroll
-            for (int r = 0; r < TL::NR; ++r) {
-                FF16::muladd(z[r], u[r], tq);
-                __builtin_amdgcn_sched_barrier(0);
-            }
+        for (int k = 0; k < NZ; ++k) {
+            q[k] = live[k] && ut != t[k] ? cload(a.qlog + (t[k] ^ ut)) : kQZero;
+            if (q[k] != kQZero && q[k] != kQOne) mulmask |= 1u << k;
         }
+        // z_k ^= q_k * U for the outputs in the (wave-uniform) mask, one set of selectors per piece
+        static_for<1, (1 << NZ)>([&](auto M) {
+            constexpr unsigned mask = decltype(M)::value;
+            if (mulmask == mask) {
+                FF16::Tab tq[NZ];
+                static_for<0, NZ>([&](auto K) {
+                    if constexpr ((mask >> K.value) & 1u) tq[K.value] = FF16::tab(a.tabs, q[K.value]);
+                });
+#pragma unroll
+                for (int r = 0; r < TL::NR; ++r) {
+                    const FF16::Sel sl = FF16::sel(u[r]);
+                    static_for<0, NZ>([&](auto K) {
+                        if constexpr ((mask >> K.value) & 1u) FF16::muladd_sel(z[K.value][r], sl, tq[K.value]);
+                    });
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+        });
+#pragma unroll
+        for (int k = 0; k < NZ; ++k)
+            if (q[k] == kQOne) TL::xor_into(z[k], u);
         // the formal derivative's low bits: D_lo U_t (rs_device.h derivative_add)
-        if (ut == t)
-            TL::derivative_add(z, [&](int r, uint32_t* out) { out[0] = u[r][0]; out[1] = u[r][1]; }, w, lane, lds);
+#pragma unroll
+        for (int k = 0; k < NZ; ++k)
+            if (live[k] && ut == t[k])
+                TL::derivative_add(z[k], [&](int r, uint32_t* out) { out[0] = u[r][0]; out[1] = u[r][1]; }, w, lane,
+                                   lds);
         ut = next;
     }
-    LogTabs16Stage<NT, (1u << T)> ls;
-    ls.load(a.tabs, a.reveal_logs + (t << T));  // in flight during the FFT
-    TL::fft(z, w, lane, lds, PieceSpace{0, 0, t << T}, LdsWindow16{fset, t << T, 0}, AllLive{});
-    __syncthreads();  // every wave is past the FFT's last exchange
-    ls.store(rvl);
-    // lost original at p = m + i: work[i] = z[p] * exp(-el[p])  (LeopardFF16.cpp:1771-1773)
-    auto pos = [&](int r) { return (t << T) + TL::piece(0, r, w); };
-    uint64_t po[TL::NR];
-    lane_ptrs(po, a.out, [&](int r) { return pos(r) >= a.m ? min(pos(r) - a.m, a.K - 1) : 0u; });
-    __syncthreads();
-    if (!cl.live) return;
+    STAMP16(2);
+    static_for<0, NZ>([&](auto K) {
+        constexpr int k = decltype(K)::value;
+        if (!live[k]) return;
+        const unsigned tk = t[k];
+        LogTabs16Stage<NT, (1u << T)> ls;
+        ls.load(a.tabs, a.reveal_logs + (tk << T));  // in flight during the FFT
+        // (the FFT's first exchange starts with a barrier: the previous output's reveal is done with rvl)
+        TL::fft(z[k], w, lane, lds, PieceSpace{0, 0, tk << T}, LdsWindow16{fset(k), tk << T, 0}, AllLive{});
+        __syncthreads();  // every wave is past the FFT's last exchange
+        STAMP16(3);
+        ls.store(rvl);
+        // lost original at p = m + i: work[i] = z[p] * exp(-el[p])  (LeopardFF16.cpp:1771-1773)
+        auto pos = [&](int r) { return (tk << T) + TL::piece(0, r, w); };
+        const uint32_t ew = a.erased_dev[(tk << 3) + (w >> (5 - R))];  // layout 0: one word a lane
+        uint64_t po[TL::NR];
+        lane_ptrs(po, a.out, [&](int r) { return pos(r) >= a.m ? min(pos(r) - a.m, a.K - 1) : 0u; });
+        __syncthreads();
+        if (cl.live) {
 #pragma unroll
-    for (int r = 0; r < TL::NR; ++r) {
-        const unsigned p = pos(r), tp = TL::piece(0, r, w);
-        if (p >= a.m && p < a.m + a.K && ((ew >> (tp & 31)) & 1u)) {
-            asm volatile("" ::: "memory");
-            uint32_t o[2];
-            FF16::mul(o, z[r], FF16::tab_lds(rvl + tab16_slot(tp)));
-            st_unit(reinterpret_cast<uint8_t*>(po[r]), cl.off, o);
+            for (int r = 0; r < TL::NR; ++r) {
+                const unsigned p = pos(r), tp = TL::piece(0, r, w);
+                if (p >= a.m && p < a.m + a.K && ((ew >> (tp & 31)) & 1u)) {
+                    asm volatile("" ::: "memory");
+                    uint32_t o[2];
+                    FF16::mul(o, z[k][r], FF16::tab_lds(rvl + tab16_slot(tp)));
+                    st_unit(reinterpret_cast<uint8_t*>(po[r]), cl.off, o);
+                }
+            }
         }
-    }
+    });
+    STAMP16(4);
 }
 
 template <class Kern>
@@ -387,10 +448,12 @@ hipError_t launch16n(Kern* fn, dim3 grid, unsigned threads, size_t lds_bytes, co
     return hipLaunchKernel(reinterpret_cast<const void*>(fn), grid, dim3(threads), params, lds_bytes, s);
 }
 
-constexpr int kDecR = 3, kDecLW = 16;
+constexpr int kDecR = 3, kDecLW = 16, kDecNZ = LAMD_DEC16N_NZ;
 using DecTL = Tile<FF16, 8, kDecR, 1, kDecLW, 0, lg_bits(kDecLW)>;
 constexpr size_t kDecLds = (DecTL::kXchDwords + tab16_set_dwords(8)) * 4;
+constexpr size_t kDecFinLds = (DecTL::kXchDwords + kDecNZ * tab16_set_dwords(8)) * 4;
 static_assert(kDecLds <= 160 * 1024 / 3, "three workgroups per CU");
+static_assert(kDecFinLds <= 160 * 1024 / 2, "two workgroups per CU");
 static_assert(tab16_slot(256) <= DecTL::kXchDwords, "log tables fit the exchange area");
 }  // namespace
 
@@ -419,8 +482,9 @@ hipError_t launch_decode16_small_lo(const DecArgs& a, hipStream_t s) {
 hipError_t launch_decode16_small_fin(const DecArgs& a, hipStream_t s) {
     const unsigned strips = unsigned((a.nunits + kDecLW - 1) / kDecLW);
     const unsigned groups = (strips + 7) / 8;  // strips dealt 8 at a time, one per XCD
-    return launch16n(&k_dec16n_fin<kDecR, kDecLW>, dim3(groups * 8 * a.nout), threads_n<8, kDecR, kDecLW>(), kDecLds,
-                     a, s);
+    const unsigned ngrp = (a.nout + kDecNZ - 1) / kDecNZ;
+    return launch16n(&k_dec16n_fin<kDecR, kDecLW, kDecNZ>, dim3(groups * 8 * ngrp), threads_n<8, kDecR, kDecLW>(),
+                     kDecFinLds, a, s);
 }
 
 }  // namespace lamd

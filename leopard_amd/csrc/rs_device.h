@@ -348,6 +348,30 @@ struct LdsSkew8 {
 struct LdsSkew8NoZero : LdsSkew8 {
     LDEV constexpr bool zero(unsigned) const { return false; }
 };
+// The dense GF(2^8) tiles (K = R = m, one chunk, PieceSpace{0, 0, 0}): the
+// skew base is a compile-time constant, so in the layout that holds the top
+// tile bits (kLast: every bit above a layer's bit is a register bit) the skew
+// of every butterfly group is known at compile time, and the groups whose skew
+// is zero (FFTSkew[2^k - 1] = 0, LeopardFF8.cpp:496-538) compile to the
+// reference's XOR-only butterfly with no branch: at skew base -1 that is 7 of
+// the 24 multiplies per lane of layers 5, 4, 3 (6 of 16 for layers 4, 5),
+// the same in every wave.  In the other layouts a group's skew depends on the
+// wave index, so there every butterfly is multiplied (LdsSkew8NoZero).
+template <int kOff>
+struct LdsSkew8Fixed : LdsSkew8NoZero {
+    static constexpr bool kStaticOffset = true;
+    static constexpr int kOffset = kOff;
+    LDEV FF8::Tab table(unsigned cidx) const { return tabs.at(kOff + int(cidx)); }
+};
+template <class W, class = void>
+struct StaticOffsetOf {
+    static constexpr bool value = false;
+};
+template <class W>
+struct StaticOffsetOf<W, std::void_t<decltype(W::kStaticOffset)>> {
+    static constexpr bool value = W::kStaticOffset;
+};
+
 template <class F>
 struct GlobalWindow {
     const uint32_t* sk = nullptr;
@@ -691,7 +715,30 @@ struct Tile {
                 }
             }
         };
-        if constexpr (F::kDw == 1) {
+        if constexpr (F::kDw == 1 && StaticOffsetOf<Win>::value && LAY == kLast) {
+            // dense tile, top layout: zero-skew groups known at compile time
+            // (LdsSkew8Fixed; piece space {0, 0, 0}, wave bits below the layer)
+            constexpr int KB = NG < LAMD_FF8_KB ? NG : LAMD_FF8_KB;
+            static_for<0, NG / KB>([&](auto BI) {
+                constexpr int g0 = decltype(BI)::value * KB;
+                typename F::Tab tabs[KB];
+                asm volatile("" ::: "memory");
+                static_for<0, KB>([&](auto GI) {
+                    constexpr int g = (g0 + GI.value) * 2 * half;
+                    constexpr unsigned cidx = ((unsigned(g << lo(LAY)) >> L) | 1u) << L;
+                    constexpr int j = Win::kOffset + int(cidx);
+                    if constexpr (((j + 1) & j) != 0) tabs[GI.value] = win.table(cidx);
+                });
+                static_for<0, KB>([&](auto GI) {
+                    constexpr int g = (g0 + GI.value) * 2 * half;
+                    constexpr unsigned cidx = ((unsigned(g << lo(LAY)) >> L) | 1u) << L;
+                    constexpr int j = Win::kOffset + int(cidx);
+                    if constexpr (((j + 1) & j) == 0) xor_group(g);
+                    else group(g, tabs[GI.value]);
+                });
+                __builtin_amdgcn_sched_barrier(0);
+            });
+        } else if constexpr (F::kDw == 1) {
             // FF8 (5-dword tables): read every table of the layer, then let the
             // scheduler interleave the layer's independent butterflies (ILP).
             // At most 4 tables (20 VGPRs) live at a time.

@@ -99,9 +99,6 @@ constexpr uint32_t kOneWgPerCuUnits = 256 * 64;  // 256 CUs x one 64-dword strip
 #ifndef LAMD_PRIO_LOADS
 #define LAMD_PRIO_LOADS 0
 #endif
-#ifndef LAMD_DENSE_ZERO_CHECK
-#define LAMD_DENSE_ZERO_CHECK 0
-#endif
 // Window of the pruned (non-dense) tiles: LAMD_FF8_ZERO_CHECK=1 keeps the
 // XOR-only branch for zero skews (rs_device.h: LdsSkew8NoZero)
 #ifndef LAMD_FF8_ZERO_CHECK
@@ -312,16 +309,11 @@ LDEV void ff8_enc(const A& a) {
     Skew8Win win{{tabs}};
     if constexpr (kDense) {
         // encode: IFFT skew base m - 1, FFT base -1; inverse: the other way round
-#if LAMD_DENSE_ZERO_CHECK
-        LdsSkew8 dwin{tabs};  // experiments: the XOR-only shortcut of zero skews
-#else
-        LdsSkew8NoZero dwin{{tabs}};
-#endif
-        dwin.stage(nullptr, kForm == kFormDenseDec ? -1 : int(m - 1));
-        ifft(dwin, AllLive{});
+        constexpr int kIfftOff = kForm == kFormDenseDec ? -1 : int(m - 1);
+        constexpr int kFftOff = kForm == kFormDenseDec ? int(m - 1) : -1;
+        ifft(LdsSkew8Fixed<kIfftOff>{{{tabs}}}, AllLive{});
         TL::fused_top(x, FF8::tab_at(a.fused));
-        dwin.stage(nullptr, kForm == kFormDenseDec ? int(m - 1) : -1);
-        fft(dwin, AllLive{});
+        fft(LdsSkew8Fixed<kFftOff>{{{tabs}}}, AllLive{});
     } else if constexpr (!kMulti) {
         win.stage(nullptr, int(m - 1));
         ifft(win, lane_pred<G>(BelowLive{a.K}));

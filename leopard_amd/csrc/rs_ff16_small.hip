@@ -35,7 +35,7 @@ __device__ uint64_t* g_stamps16;
     do {                                                                                                 \
         const uint64_t t_ = __builtin_amdgcn_s_memrealtime();                                            \
         if ((threadIdx.x & 63) == 0)                                                                     \
-            g_stamps16[(uint64_t(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8 + (k)] = t_; \
+            g_stamps16[kStampBase + ((uint64_t(blockIdx.y) * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8 + (k)] = t_; \
     } while (0)
 #else
 #define STAMP16(k) \
@@ -140,6 +140,7 @@ __global__ void __launch_bounds__((threads_n<T, R, LW>()), 4) k_enc16n(EncArgs a
             for (int k = 0; k < TL::U; ++k) dst[r][k] = ok ? src[r][k] : 0u;
         }
     };
+    [[maybe_unused]] constexpr uint64_t kStampBase = 0;
     STAMP16(0);
     {
         Tabs16Stage<NT, T> st;
@@ -239,6 +240,8 @@ __global__ void __launch_bounds__((threads_n<8, R, LW>()), 4) k_dec16n_lo(DecArg
     constexpr unsigned NT = threads_n<T, R, LW>();
     const unsigned y = blockIdx.y;
     if (!pyr_bit(a.present_pyr, T, y)) return;  // nothing received in this tile: U_y = 0, pass 2 skips it
+    [[maybe_unused]] constexpr uint64_t kStampBase = 0;
+    STAMP16(0);
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t* set = lds + TL::kXchDwords;
     uint32_t* scl = lds;  // the scale tables share the exchange area: used before the first transpose
@@ -272,6 +275,7 @@ __global__ void __launch_bounds__((threads_n<8, R, LW>()), 4) k_dec16n_lo(DecArg
     st.store(set);
     ls.store(scl);
     __syncthreads();
+    STAMP16(1);
     // scale by exp(el[p]) (the zero table for absent positions)
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) {
@@ -281,13 +285,16 @@ __global__ void __launch_bounds__((threads_n<8, R, LW>()), 4) k_dec16n_lo(DecArg
 #pragma unroll
         for (int k = 0; k < TL::U; ++k) asm volatile("" : "+v"(x[r][k]));
     }
+    STAMP16(2);
     TL::ifft(x, w, lane, lds, ps, LdsWindow16{set, y << T, 0}, AllLive{});
+    STAMP16(3);
     if (!cl.live) return;
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) {
         const uint64_t row = ps.global(TL::piece(TL::kLast, r, w));
         st_unit(a.a_out.base + row * a.a_out.stride + a.a_out.off, cl.off, x[r]);
     }
+    STAMP16(4);
 }
 
 // Pass 2 over NZ consecutive output tiles per workgroup: every U tile is read
@@ -326,6 +333,7 @@ __global__ void __launch_bounds__((threads_n<8, R, LW>()), LAMD_DEC16N_FIN_WAVES
         any |= live[k];
     }
     if (!any) return;
+    [[maybe_unused]] constexpr uint64_t kStampBase = 1ull << 22;
     STAMP16(0);
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t* rvl = lds;  // the reveal tables go to the exchange area once an FFT is done with it

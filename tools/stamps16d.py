@@ -33,14 +33,18 @@ stamps.zero_()
 assert lib.leo_decode(b, k, r, dwc, po, pr, pd) == 0
 torch.cuda.synchronize()
 NS = 5
-v = stamps.view(-1, 8)[:, :NS].cpu().double()
-v = v[v[:, 0] > 0]
-t0 = v[:, 0].min()
-print(f"{k}+{r} x {b}, {loss} lost: {len(v)} waves stamped")
-for kk in range(NS):
-    col = ((v[:, kk] - t0) / 100.0).sort()[0]
-    n = len(col)
-    print(f"stamp {kk}: min {col[0]:7.2f} p10 {col[n//10]:7.2f} med {col[n//2]:7.2f} p90 {col[n*9//10]:7.2f} max {col[-1]:7.2f} us")
-d = (v[:, 1:] - v[:, :-1]) / 100.0
-print("per-wave phase durations (median us): tables+first U, q-loop, FFT, reveal+store:",
-      [round(float(x), 2) for x in d.median(dim=0)[0]])
+allv = stamps.view(-1, 8)[:, :NS].cpu().double()
+t0 = allv[allv[:, 0] > 0][:, 0].min()
+for name, lo_, hi_, phases in (("pass 1 (k_dec16n_lo)", 0, (1 << 22) // 8,
+                                "loads+tables, scale, IFFT, store"),
+                               ("pass 2 (k_dec16n_fin)", (1 << 22) // 8, None,
+                                "tables+first U, fold loop, FFT, reveal+store")):
+    v = allv[lo_:hi_]
+    v = v[v[:, 0] > 0]
+    print(f"{name}: {k}+{r} x {b}, {loss} lost: {len(v)} waves stamped")
+    for kk in range(NS):
+        col = ((v[:, kk] - t0) / 100.0).sort()[0]
+        n = len(col)
+        print(f"  stamp {kk}: min {col[0]:7.2f} p10 {col[n//10]:7.2f} med {col[n//2]:7.2f} p90 {col[n*9//10]:7.2f} max {col[-1]:7.2f} us")
+    d = (v[:, 1:] - v[:, :-1]) / 100.0
+    print(f"  per-wave phase durations (median us): {phases}:", [round(float(x), 2) for x in d.median(dim=0)[0]])

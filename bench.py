@@ -493,6 +493,36 @@ def configs4_sharded(args, leo, torch, device, barrier, rank, world, max_over_ra
                         "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                         "frac": round(algo / world / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
                         "algorithmic_bytes_per_step": algo}}
+    # configs[3] per call on this rank's columns: encode alone, decode alone (HIP events on the
+    # call stream), with the kernels the library runs and the committed PMC traffic (full width)
+    def timed(fn, reps=3):
+        fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            fn()
+        e1.record(stream)
+        e1.synchronize()
+        return e0.elapsed_time(e1) / reps
+
+    def enc():
+        if lib.leo_amd_encode_slice(b, off, size, k, r, wc, po, pw) != 0:
+            raise RuntimeError(leo.last_error())
+
+    def dec():
+        if lib.leo_amd_decode_slice(b, off, size, k, r, dwc, pn, pr, pd) != 0:
+            raise RuntimeError(leo.last_error())
+
+    kern = kernels_for(k, r, size, k)
+    per = {}
+    for kind, fn in (("encode", enc), ("decode", dec)):
+        cms = timed(fn)
+        algo1 = (k + r) * size
+        t = pmc_traffic(kind, k, r, b) if size == b else {}
+        per[kind] = {"ms": round(cms, 3), "kernel": kern[kind], "achieved": round(algo1 / cms / 1e6, 2),
+                     "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(algo1 / cms / 1e6 / HBM_PEAK_GBPS, 4),
+                     "algorithmic_bytes": algo1, "traffic": t.get("bytes"), "traffic_source": t.get("source")}
+    res["per_call"] = per
     if n1_ms is not None:
         res["one_gpu_ms_per_step"] = round(n1_ms, 3)
         res["speedup_vs_one_gpu"] = round(n1_ms / ms, 3)
@@ -565,12 +595,22 @@ def run_shape(leo, torch, device, k, r, nbytes, loss, n=3):
     ok = all(bool(torch.equal(st[2].index_select(0, idx), st[0].index_select(0, idx))) for st in sets)
     inb = k * nbytes
     field = "GF(2^8)" if dwc <= 256 else "GF(2^16)"
+    kern = kernels_for(k, r, nbytes, loss)
+
+    def roof(kind, us, algo):  # roofline of the call's kernels, PMC traffic when committed for this shape
+        t = pmc_traffic(kind, k, r, nbytes)
+        return {"bound": "hbm", "kernel": kern.get(kind) if isinstance(kern, dict) else None,
+                "achieved": round(algo / us / 1e3, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": round(algo / us / 1e3 / HBM_PEAK_GBPS, 4), "algorithmic_bytes": algo,
+                "traffic": t.get("bytes"), "traffic_source": t.get("source")}
     res = {"workload": f"{k}+{r} x {nbytes} B, {field}, {loss} originals lost", "encode_GBps": round(inb / te / 1e9, 3),
            "decode_GBps": round(inb / td / 1e9, 3), "encode_decode_GBps": round(inb / (te + td) / 1e9, 3),
            "encode_us": round(te * 1e6, 2), "decode_us": round(td * 1e6, 2), "roundtrip_ok": ok,
-           "buffer_sets": nsets, "kernels": kernels_for(k, r, nbytes, loss),
+           "buffer_sets": nsets, "kernels": kern,
            "roofline_frac": {"encode": round((k + r) * nbytes / te / 1e9 / HBM_PEAK_GBPS, 4),
-                             "decode": round((k + loss) * nbytes / td / 1e9 / HBM_PEAK_GBPS, 4)}}
+                             "decode": round((k + loss) * nbytes / td / 1e9 / HBM_PEAK_GBPS, 4)},
+           "roofline": {"encode": roof("encode", te * 1e6, (k + r) * nbytes),
+                        "decode": roof("decode", td * 1e6, (k + loss) * nbytes)}}
     del sets
     torch.cuda.empty_cache()
     return res

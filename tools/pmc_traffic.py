@@ -40,24 +40,46 @@ def main():
         args = args[2:]
     k, r, b = (int(x) for x in args[:3])
     dirs = args[3:]
+    loss = calls = None
+    while dirs and dirs[0].startswith("--"):
+        opt, val = dirs[0][2:].split("=", 1)
+        if opt == "loss":  # originals lost in the decode (its algorithmic bytes)
+            loss = int(val)
+        elif opt == "calls":  # calls of each kind in the run: bytes per call = all dispatches' bytes / calls
+            calls = int(val)
+        dirs = dirs[1:]
+    # per kernel (a call of a multi-pass path launches each of its kernels once):
+    # average over dispatches, then the call's bytes = sum over its kernels
     vals = defaultdict(lambda: defaultdict(list))
-    names = {}
     for d in dirs:
         for f in glob.glob(d.rstrip("/") + "/**/*counter_collection.csv", recursive=True):
             for row in csv.DictReader(open(f)):
                 kind = kernel_kind(row["Kernel_Name"])
                 if kind is None:
                     continue
-                names[kind] = re.sub(r"^.*::(k_\w+<[^>]*>).*$", r"\1", row["Kernel_Name"])
-                vals[kind][row["Counter_Name"]].append(float(row["Counter_Value"]))
+                name = re.sub(r"^.*::(k_\w+<[^>]*>).*$", r"\1", row["Kernel_Name"])
+                vals[(kind, name)][row["Counter_Name"]].append(float(row["Counter_Value"]))
     out = {}
-    for kind, cs in vals.items():
+    for (kind, name), cs in sorted(vals.items()):
         fetch = sum(cs["FETCH_SIZE"]) / len(cs["FETCH_SIZE"])
         write = sum(cs["WRITE_SIZE"]) / len(cs["WRITE_SIZE"])
-        out[kind] = {"kernel": names[kind], "FETCH_SIZE_KiB": round(fetch, 1), "WRITE_SIZE_KiB": round(write, 1),
-                     "dispatches": len(cs["FETCH_SIZE"]),
-                     "hbm_bytes_per_launch": int((2 * fetch + write) * 1024),
-                     "algorithmic_bytes_per_launch": objects * (k + r) * b}
+        e = out.setdefault(kind, {"kernel": "", "FETCH_SIZE_KiB": 0.0, "WRITE_SIZE_KiB": 0.0, "dispatches": 0,
+                                  "hbm_bytes_per_launch": 0})
+        e["kernel"] = (e["kernel"] + " + " if e["kernel"] else "") + name
+        e["FETCH_SIZE_KiB"] = round(e["FETCH_SIZE_KiB"] + fetch, 1)
+        e["WRITE_SIZE_KiB"] = round(e["WRITE_SIZE_KiB"] + write, 1)
+        e["dispatches"] += len(cs["FETCH_SIZE"])
+        if calls:  # several dispatches of a kernel per call (column slices): total / calls
+            e["hbm_bytes_per_launch"] += int((2 * sum(cs["FETCH_SIZE"]) + sum(cs["WRITE_SIZE"])) * 1024 / calls)
+        else:
+            e["hbm_bytes_per_launch"] += int((2 * fetch + write) * 1024)
+    for kind, e in out.items():
+        # encode (K + R) * B; decode (K_surv + R_recv + lost) * B, which is
+        # (K + loss) * B when exactly `loss` recovery pieces are received (the benchmark's pattern)
+        if kind == "decode" and loss is not None:
+            e["algorithmic_bytes_per_launch"] = objects * (k + loss) * b
+        else:
+            e["algorithmic_bytes_per_launch"] = objects * (k + r) * b
     key = f"{k}+{r}x{b}" + (f"/batch{objects}" if objects > 1 else "")
     print(json.dumps({"workloads": {key: out},
                       "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes; (2*FETCH+WRITE) KiB"},

@@ -405,6 +405,16 @@ struct LdsWindow16 {
     LDEV void stage(const uint32_t*, int) {}
 };
 constexpr size_t kTab16LdsDwords = 20;
+// A set staged at skew base kOff with hi_fixed = 0 and l0 = kL0: in the layout
+// holding the top tile bits, a group's skew position is known at compile time,
+// and the zero-skew groups run the XOR-only butterfly with no branch (as
+// LdsSkew8Fixed for GF(2^8)).  At skew base -1 that is group 0 of every layer.
+template <int kOff, unsigned kL0>
+struct LdsWindow16Static : LdsWindow16 {
+    static constexpr bool kStaticOffset = true;
+    static constexpr int kOffset = kOff;
+    static constexpr unsigned kLowBits = kL0;
+};
 
 // Cooperative global -> LDS copy of one set of 2^T FF16 skew tables (see
 // LdsWindow16), split like TabStage8: load() issues the global loads (ahead of
@@ -787,6 +797,22 @@ struct Tile {
             static_for<0, NG>([&](auto GI) {
                 constexpr int g = decltype(GI)::value * 2 * half;
                 asm volatile("" ::: "memory");
+                if constexpr (StaticOffsetOf<Win>::value && LAY == kLast) {
+                    // LdsWindow16Static: wave bits below the layer, hi_fixed = 0
+                    constexpr unsigned cidx = ((unsigned(g << lo(LAY)) >> L) | 1u) << (L + Win::kLowBits);
+                    constexpr int j = Win::kOffset + int(cidx);
+                    if constexpr (((j + 1) & j) == 0) {
+                        if (live(g)) {
+                            xor_group(g);
+#pragma unroll
+                            for (int jj = 0; jj < 2 * half; ++jj)
+#pragma unroll
+                                for (int k = 0; k < U; ++k) asm volatile("" : "+v"(x[g + jj][k]));
+                        }
+                        __builtin_amdgcn_sched_barrier(0);
+                        return;
+                    }
+                }
                 if (live(g)) {
                     group(g, table(g));
                     // materialise the group's outputs here: otherwise the

@@ -182,7 +182,7 @@ __global__ void __launch_bounds__((threads_n<T, R, LW>()), 4) k_enc16n(EncArgs a
         st.load(a.sktab, -1, 0, 0);
         st.store(fset);
         __syncthreads();
-        TL::template fft<true>(acc, w, lane, lds, ps, LdsWindow16{fset, 0, 0}, AllLive{});
+        TL::template fft<true>(acc, w, lane, lds, ps, LdsWindow16Static<-1, 0>{{fset, 0, 0}}, AllLive{});
     }
     TL::pin(acc);
     STAMP16(6);

@@ -304,7 +304,8 @@ __global__ void __launch_bounds__(threads16(T, R), LAMD_HI_WAVES) k_enc_hi(EncAr
     const bool live = cl.live;
     const unsigned m = 1u << a.Tm;
     const PieceSpace ps{blockIdx.y, kLoBits, 0};
-    const LdsWindow16 iwin{iset, 0, kLoBits}, fwin{fset, 0, kLoBits};
+    const LdsWindow16 iwin{iset, 0, kLoBits};
+    const LdsWindow16Static<-1, kLoBits> fwin{{fset, 0, kLoBits}};  // staged at skew base -1
     typename TL::Reg x;
     auto load_chunk = [&](unsigned c) {
         const unsigned base = c * m;
@@ -479,7 +480,7 @@ __global__ void __launch_bounds__(threads16(T, R), LAMD_HI_WAVES) k_dec_hi(DecAr
     }
     st.store(set);
     __syncthreads();
-    const LdsWindow16 win{set, 0, kLoBits};
+    const LdsWindow16Static<-1, kLoBits> win{{set, 0, kLoBits}};  // staged at skew base -1
     TL::template ifft<true>(v, w, lane, lds, ps, win, prune16(Pyr16Live{a.present_pyr}));
     TL::derivative_swaptop(v, w, lane, lds, true);
     TL::template fft<true>(v, w, lane, lds, ps, win, prune16(Pyr16Live{a.needed_pyr}));
@@ -522,7 +523,8 @@ __global__ void __launch_bounds__(threads16(T, R), LAMD_HI_WAVES) k_dec_hi_half(
     sl.store(lset);
     sh.store(hset);
     __syncthreads();
-    TL::template ifft<true>(v, w, lane, lds, low, LdsWindow16{lset, 0, kLoBits}, prune16(Pyr16Live{a.present_pyr}));
+    TL::template ifft<true>(v, w, lane, lds, low, LdsWindow16Static<-1, kLoBits>{{lset, 0, kLoBits}},
+                            prune16(Pyr16Live{a.present_pyr}));
     TL::fused_top(v, FF16::tab(a.tabs, cload(a.fused)));
     TL::template fft<true>(v, w, lane, lds, high, LdsWindow16{hset, a.m, kLoBits}, prune16(Pyr16Live{a.needed_pyr}));
     if (live)

@@ -726,8 +726,9 @@ struct Tile {
             }
         };
         if constexpr (F::kDw == 1 && StaticOffsetOf<Win>::value && LAY == kLast) {
-            // dense tile, top layout: zero-skew groups known at compile time
-            // (LdsSkew8Fixed; piece space {0, 0, 0}, wave bits below the layer)
+            // top layout of a transform at a compile-time skew base: zero-skew
+            // groups known at compile time (LdsSkew8Fixed; piece space
+            // {0, 0, 0}, wave bits below the layer)
             constexpr int KB = NG < LAMD_FF8_KB ? NG : LAMD_FF8_KB;
             static_for<0, NG / KB>([&](auto BI) {
                 constexpr int g0 = decltype(BI)::value * KB;
@@ -743,8 +744,10 @@ struct Tile {
                     constexpr int g = (g0 + GI.value) * 2 * half;
                     constexpr unsigned cidx = ((unsigned(g << lo(LAY)) >> L) | 1u) << L;
                     constexpr int j = Win::kOffset + int(cidx);
-                    if constexpr (((j + 1) & j) == 0) xor_group(g);
-                    else group(g, tabs[GI.value]);
+                    if (live(g)) {
+                        if constexpr (((j + 1) & j) == 0) xor_group(g);
+                        else group(g, tabs[GI.value]);
+                    }
                 });
                 __builtin_amdgcn_sched_barrier(0);
             });

@@ -319,8 +319,7 @@ LDEV void ff8_enc(const A& a) {
         ifft(win, lane_pred<G>(BelowLive{a.K}));
         STAMP(3);
         TL::fused_top(x, FF8::tab_at(a.fused));
-        win.stage(nullptr, -1);
-        fft(win, lane_pred<G>(BelowLive{a.R}));
+        fft(LdsSkew8Fixed<-1>{{{tabs}}}, lane_pred<G>(BelowLive{a.R}));
         STAMP(4);
     } else {
         typename TL::Reg acc;
@@ -334,8 +333,7 @@ LDEV void ff8_enc(const A& a) {
             load_chunk(c);
         }
         TL::copy(x, acc);
-        win.stage(nullptr, -1);
-        fft(win, lane_pred<G>(BelowLive{a.R}));
+        fft(LdsSkew8Fixed<-1>{{{tabs}}}, lane_pred<G>(BelowLive{a.R}));
     }
     TL::pin(x);
     uint64_t pp[TL::NR];
@@ -500,8 +498,8 @@ LDEV void ff8_dec(const Ff8DecArgs& a) {
     STAMP(2);
     // scale by exp(el) (absent pieces stay zero)
     scale_batched<TL>(v, ltab, [&](int r) { return el_at(pos(r)); }, [&](int r) { return present(pos(r), 0); });
-    Skew8Win win{{sk}};
-    win.stage(nullptr, -1);
+    // decoder skew base -1 (LeopardFF8.cpp:1880, 1903), piece space {0, 0, 0}
+    const LdsSkew8Fixed<-1> win{{{sk}}};
     // IFFT and FFT without their top layers around swap_top + D_low (see
     // Tile::derivative_swaptop): the same map as IFFT, (I + D), FFT
     if constexpr (pipe8(NA)) {
@@ -595,7 +593,7 @@ LDEV void ff8_dec_half(const Ff8DecArgs& a) {
     win.stage(nullptr, -1);  // decoder skew base (LeopardFF8.cpp:1880, 1903)
     // both top layers (single skews m/2 - 1 and m + m/2 - 1) as one butterfly
     // with their sum, the encoder's chunk-0 fused table (Tile::fused_top)
-    TL::template ifft<true>(v, w, lane, lds, low, win, present);
+    TL::template ifft<true>(v, w, lane, lds, low, LdsSkew8Fixed<-1>{{{sk}}}, present);
     TL::fused_top(v, FF8::tab_at(a.fused));
     TL::template fft<true>(v, w, lane, lds, high, win, needed);
     TL::pin(v);
@@ -675,7 +673,7 @@ LDEV void ff8_dec_split(const Ff8DecArgs& a) {
     TL::derivative_add(y, [&](int r, uint32_t* out) { out[0] = h[r][0]; }, w, lane, lds);
     // x <- I_L(x * exp(el)) ^ y, then F_H
     scale_batched<TL>(x, ltab, [&](int r) { return el_at(lpos(r)); }, [&](int r) { return present(lpos(r), 0); });
-    TL::template ifft<false>(x, w, lane, lds, low, win, present);
+    TL::template ifft<false>(x, w, lane, lds, low, LdsSkew8Fixed<-1>{{{sk}}}, present);
     TL::xor_into(x, y);
     TL::template fft<false>(x, w, lane, lds, high, win, needed);
     TL::pin(x);

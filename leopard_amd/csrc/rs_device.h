@@ -624,9 +624,23 @@ struct Tile {
 
     static constexpr int lo(int k) { return k * R < T - R ? k * R : T - R; }
     static_assert(S == 0 || split_of(NL - 1, (1 << S) - 1) == (1u << S) - 1, "kLast: split class = low register bits");
-    // IFFT layers done in layout k: [ifft_begin(k), lo(k) + R); FFT layers: [lo(k), fft_end(k))
-    static constexpr int ifft_begin(int k) { return k == 0 ? 0 : lo(k - 1) + R; }
+    // Layers done in layout k.  FFT: [lo(k), lo(k + 1)) (the last layout up to
+    // T), i.e. every layer in the latest layout holding its bit.  IFFT: by
+    // default [lo(k - 1) + R, lo(k) + R), every layer in the earliest one; with
+    // kLate the FFT's rule, which puts the most layers in the top layout, where
+    // a transform at skew base -1 has its zero-skew groups at compile time
+    // (LdsSkew8Fixed, LdsWindow16Static; measured: the decoders gain, the
+    // encoders' base m - 1 IFFTs lose 2-4% to the other order, r03_v12).
+    template <bool kLate>
+    static constexpr int ifft_begin(int k) { return kLate ? lo(k) : (k == 0 ? 0 : lo(k - 1) + R); }
+    template <bool kLate>
+    static constexpr int ifft_end(int k) { return kLate ? (k == NL - 1 ? T : lo(k + 1)) : lo(k) + R; }
     static constexpr int fft_end(int k) { return k == NL - 1 ? T : lo(k + 1); }
+    template <class Win>
+    static constexpr bool late_ifft() {
+        if constexpr (StaticOffsetOf<Win>::value) return Win::kOffset == -1;
+        else return false;
+    }
 
     // tile piece held in register r by wave w in layout k
     LDEV static unsigned piece(int k, int r, unsigned w) {
@@ -917,9 +931,10 @@ struct Tile {
         uint32_t pw[kMaxGroups];
     };
 
+    template <bool kLate>
     static constexpr int ifft_layout(int L) {
         int k = 0;
-        while (!(L >= ifft_begin(k) && L < lo(k) + R)) ++k;
+        while (!(L >= ifft_begin<kLate>(k) && L < ifft_end<kLate>(k))) ++k;
         return k;
     }
     static constexpr int fft_layout(int L) {
@@ -1016,15 +1031,16 @@ struct Tile {
     LDEV static void ifft_pl(Reg& x, unsigned w, unsigned lane, Ring& ring, const PieceSpace& ps, const Win& win,
                              const Pred& pred = Pred{}) {
         constexpr int NS = kSkipTop ? T - 1 : T;  // layers computed here
+        constexpr bool kL = late_ifft<Win>();
         Look cur, nxt;
-        if constexpr (NS > 0) read_look<ifft_layout(0), 0>(cur, w, ps, win, pred);
+        if constexpr (NS > 0) read_look<ifft_layout<kL>(0), 0>(cur, w, ps, win, pred);
         static_for<0, (NS > 0 ? NS : 0)>([&](auto LI) {
-            constexpr int L = decltype(LI)::value, k = ifft_layout(L);
+            constexpr int L = decltype(LI)::value, k = ifft_layout<kL>(L);
             const uint32_t live = live_mask<k, L>(cur, w, ps, pred);
-            if constexpr (L + 1 < NS) read_look<ifft_layout(L + 1), L + 1>(nxt, w, ps, win, pred);
+            if constexpr (L + 1 < NS) read_look<ifft_layout<kL>(L + 1), L + 1>(nxt, w, ps, win, pred);
             apply<true, k, L>(x, cur, live);
-            if constexpr (L + 1 < T && ifft_layout(L + 1) != k) exchange<k, ifft_layout(L + 1)>(x, w, lane, ring);
-            if constexpr (L + 1 < NS) take_look<ifft_layout(L + 1), L + 1>(cur, nxt);
+            if constexpr (L + 1 < T && ifft_layout<kL>(L + 1) != k) exchange<k, ifft_layout<kL>(L + 1)>(x, w, lane, ring);
+            if constexpr (L + 1 < NS) take_look<ifft_layout<kL>(L + 1), L + 1>(cur, nxt);
         });
         if constexpr (NS == 0 && NL > 1) exchange<0, kLast>(x, w, lane, ring);
     }
@@ -1058,8 +1074,9 @@ struct Tile {
                           const Pred& pred = Pred{}) {
         static_for<0, NL>([&](auto K) {
             constexpr int k = decltype(K)::value;
-            constexpr int end = (kSkipTop && k == NL - 1) ? T - 1 : lo(k) + R;
-            static_for<ifft_begin(k), end>(
+            constexpr bool kL = late_ifft<Win>();
+            constexpr int end = (kSkipTop && k == NL - 1) ? T - 1 : ifft_end<kL>(k);
+            static_for<ifft_begin<kL>(k), end>(
                 [&](auto L) { layer<true, k, decltype(L)::value>(x, w, ps, win, pred); });
             if constexpr (k + 1 < NL) transpose<k, k + 1>(x, w, lane, lds);
         });

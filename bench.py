@@ -99,7 +99,63 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=5.0)
     ap.add_argument("--no-secondary", action="store_true", help="skip 1000+200, B=64000 and the breadth shapes")
     ap.add_argument("--no-host", action="store_true", help="skip the host-memory (PCIe-inclusive) rate")
+    ap.add_argument("--stub", action="store_true",
+                    help="launcher test (tests/test_cpu_bench_launcher.py): ranks rendezvous, barrier and take the "
+                         "max over ranks of a stand-in time, with no GPU work")
     return ap.parse_args()
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` run without a launcher (no WORLD_SIZE): start N rank
+    processes of this script, one per GPU, and return the first non-zero exit
+    code.  They are fresh interpreters started from this one before it makes
+    any GPU call (it never makes one), with RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_* set as torch.distributed.run would set them; rank 0 prints the
+    line.  A rank that fails ends the others (they would wait at a barrier)."""
+    import socket
+    import subprocess
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc if rc >= 0 else 128 - rc
+
+
+def stub_rank(world, rank):
+    """--stub: the launcher's control plane alone (gloo rendezvous, barrier,
+    max over ranks), for the CPU test of launch_ranks."""
+    import torch.distributed as dist
+    from leopard_amd.sharding import max_over_ranks
+    if world > 1:
+        dist.init_process_group("gloo")
+        dist.barrier()
+    el = max_over_ranks(0.25 * (rank + 1))
+    ranks = [None] * world
+    if world > 1:
+        dist.all_gather_object(ranks, {"rank": rank, "pid": os.getpid()})
+        dist.destroy_process_group()
+    else:
+        ranks = [{"rank": 0, "pid": os.getpid()}]
+    if rank == 0:
+        print(json.dumps({"stub": True, "world": world, "max_over_ranks": el, "ranks": ranks}), flush=True)
 
 
 def hash_fill_cuda(torch, seed, pieces, nbytes, device):
@@ -154,19 +210,32 @@ class Sets:
 
 def main():
     args = parse()
-    import torch
-    import torch.distributed as dist
-
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))  # before anything touches a GPU
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.stub:
+        return stub_rank(world, rank)
+    import torch
+    import torch.distributed as dist
+
     if world > 1:
         dist.init_process_group("gloo")  # control plane only (barrier, max-time); no data-path collective
-    # one process per GPU; more ranks than GPUs (a functional rehearsal on a
-    # smaller box) share devices round-robin
-    gpu = local % max(1, torch.cuda.device_count())
+    # one process per GPU (device = local rank); more ranks than GPUs (a
+    # functional rehearsal on a smaller box) share devices round-robin, and the
+    # line says so (n_gpus = distinct devices, world = ranks)
+    ndev = max(1, torch.cuda.device_count())
+    gpu = local % ndev
+    if ndev >= int(os.environ.get("LOCAL_WORLD_SIZE", world)):
+        assert gpu == local, "each rank owns a distinct device"
     torch.cuda.set_device(gpu)
     device = torch.device("cuda", gpu)
+    placement = [(os.uname().nodename, gpu)]
+    if world > 1:
+        placement = [None] * world
+        dist.all_gather_object(placement, (os.uname().nodename, gpu))
+    n_devices = len(set(placement))
 
     import leopard_amd as leo
     from leopard_amd.sharding import max_over_ranks
@@ -214,7 +283,7 @@ def main():
             "metric": "device-resident encode+decode GB/s (input bytes/s) at 128+128 and 32768+32768 pieces",
             "value": head["value"],
             "unit": "GB/s",
-            "n_gpus": world,
+            "n_gpus": n_devices,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": head["ms_per_step"],
@@ -235,7 +304,15 @@ def main():
                        "objects_per_step": args.objects, "objects_per_launch": head["launch_objects"], "mode": args.mode,
                        "field": "FF8" if leo.leo_decode_work_count(k, r) <= 256 else "FF16",
                        "sharding": "objects per rank (headline); 64-byte column blocks per rank (sharded_object); "
-                                   "no collective"},
+                                   "no collective",
+                       # scalars the driver's record keeps (it drops nested objects): ranks and their devices,
+                       # and the PCIe-inclusive host rate (never `value`)
+                       "world": world, "devices": ",".join(f"{h}:{g}" for h, g in placement),
+                       "shared_devices": n_devices < world,
+                       "host_e2e_GBps": host["value"] if host else None,
+                       "host_encode_GBps": host["encode_GBps"] if host else None,
+                       "host_decode_GBps": host["decode_GBps"] if host else None,
+                       "host_registered_GBps": host["registered"]["value"] if host else None},
             "modes": head["modes"],
             "encode_GBps": round(k * nbytes / head["t_enc"] / 1e9, 3),
             "decode_GBps": round(k * nbytes / head["t_dec"] / 1e9, 3),
@@ -247,6 +324,10 @@ def main():
                          "algorithmic_bytes_per_launch": algo, "launch_us": round(t_kernel * 1e6, 3),
                          "batch_encode_us": round(head["tb_enc"] * 1e6, 3),
                          "batch_decode_us": round(head["tb_dec"] * 1e6, 3),
+                         # per-config fractions as scalars (the driver's record keeps scalars only)
+                         "single_call_us": round(s_t * 1e6, 3),
+                         "single_call_frac": round(s_algo / s_t / 1e9 / HBM_PEAK_GBPS, 4),
+                         **config_fracs(secondary, sharded, world),
                          "single_call": {"kernel": s_kind, "launch_us": round(s_t * 1e6, 3),
                                          "achieved": round(s_algo / s_t / 1e9, 2),
                                          "frac": round(s_algo / s_t / 1e9 / HBM_PEAK_GBPS, 4),
@@ -261,6 +342,29 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def config_fracs(secondary, sharded, world):
+    """Roofline fractions and times of configs[2] (1000+200 x 64 KiB, 200
+    random losses) and configs[3] (32768+32768 x 64 KiB, full loss; whole
+    object only at N = 1), flat."""
+    out = {}
+    if secondary:
+        c2 = secondary[0]
+        out.update({"configs2_encode_us": c2["encode_us"], "configs2_decode_us": c2["decode_us"],
+                    "configs2_encode_frac": c2["roofline"]["encode"]["frac"],
+                    "configs2_decode_frac": c2["roofline"]["decode"]["frac"]})
+        if len(secondary) > 3:
+            c1p = secondary[3]  # 128+128 x 64 KiB, 16 random losses (partial-loss decoder)
+            out["configs1_16loss_decode_us"] = c1p["decode_us"]
+    if sharded and world == 1:
+        pc = sharded["per_call"]
+        out.update({"configs3_encode_ms": pc["encode"]["ms"], "configs3_decode_ms": pc["decode"]["ms"],
+                    "configs3_encode_frac": pc["encode"]["frac"], "configs3_decode_frac": pc["decode"]["frac"]})
+    if sharded:
+        out["configs4_GBps"] = sharded["value"]
+        out["configs4_roundtrip_ok"] = sharded["roundtrip_ok"]
+    return out
 
 
 def headline(args, leo, torch, device, barrier, world, max_over_ranks):
@@ -462,6 +566,8 @@ def configs4_sharded(args, leo, torch, device, barrier, rank, world, max_over_ra
     step(off, size)
     torch.cuda.synchronize()
     ok = bool(torch.equal(dwork[:k, off:off + size], data[:, off:off + size]))
+    if world > 1:  # every rank's columns round-trip
+        ok = max_over_ranks(0.0 if ok else 1.0) == 0.0
     nsteps = args.sharded_steps or max(1, min(args.steps, 10))
     step(off, size)
     barrier()

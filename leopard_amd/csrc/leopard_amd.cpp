@@ -19,6 +19,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include <immintrin.h>
@@ -86,6 +87,10 @@ struct DeviceTables {
     uint32_t* qlog16 = nullptr;  // high part of the small FF16 decoder (gf_tables.h: build_high_q16)
     uint8_t* zeros = nullptr;   // zero page
     hipStream_t svc = nullptr;  // library-owned stream for releasing workspace memory
+    // Library-owned stream-ordered memory pool of the workspaces: trimming it
+    // (release_device_memory) never touches the application's own cached
+    // stream-ordered memory in the device's default pool.
+    hipMemPool_t pool = nullptr;
     bool ready = false;
 };
 
@@ -124,6 +129,16 @@ LeopardResult ensure_device(int dev, DeviceTables** out) {
         HIP_OK(hipMalloc(reinterpret_cast<void**>(&d.zeros), 4096), "zero page");
         HIP_OK(hipMemset(d.zeros, 0, 4096), "zero page");
         HIP_OK(hipStreamCreateWithFlags(&d.svc, hipStreamNonBlocking), "service stream");
+        hipMemPoolProps props;
+        std::memset(&props, 0, sizeof(props));
+        props.allocType = hipMemAllocationTypePinned;
+        props.handleTypes = hipMemHandleTypeNone;
+        props.location.type = hipMemLocationTypeDevice;
+        props.location.id = dev;
+        HIP_OK(hipMemPoolCreate(&d.pool, &props), "workspace memory pool");
+        // keep freed blocks for reuse until release_device_memory trims the pool
+        uint64_t keep = UINT64_MAX;
+        HIP_OK(hipMemPoolSetAttribute(d.pool, hipMemPoolAttrReleaseThreshold, &keep), "pool release threshold");
         d.ready = true;
     }
     *out = &d;
@@ -149,9 +164,15 @@ struct DeviceGuard {
     }
 };
 
+// Stream-ordered allocation from the library's pool of device dev.
+hipError_t pool_alloc(void** p, size_t bytes, int dev, hipStream_t s) {
+    return hipMallocFromPoolAsync(p, bytes, g_dev[dev].pool, s);
+}
+
 // Frees stream-ordered allocations that nothing uses any more on the device's
-// service stream and trims the default pool, so that the memory is free again
-// (hipMemGetInfo) when this returns.
+// service stream and trims the library's pool (only its own: the application's
+// allocations are elsewhere), so that the memory is free again (hipMemGetInfo)
+// when this returns.
 void release_device_memory(int dev, std::initializer_list<void*> ptrs) {
     hipStream_t svc = dev >= 0 && dev < int(g_dev.size()) ? g_dev[dev].svc : nullptr;
     bool any = false;
@@ -162,8 +183,7 @@ void release_device_memory(int dev, std::initializer_list<void*> ptrs) {
         }
     if (!any) return;
     (void)hipStreamSynchronize(svc);
-    hipMemPool_t pool = nullptr;
-    if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess && pool) (void)hipMemPoolTrimTo(pool, 0);
+    if (svc && g_dev[dev].pool) (void)hipMemPoolTrimTo(g_dev[dev].pool, 0);
 }
 
 // Scratch of one (thread, device, stream): device arena plus a pinned host
@@ -219,6 +239,30 @@ struct Workspace {
     // Device rows of a host call staged by direct SDMA copies (run_host_direct).
     uint8_t* direct = nullptr;
     size_t direct_size = 0;
+    // GF(2^8) error locators by erasure pattern (k_el8's outputs): kEl8Slots
+    // slots of 256 bytes on the device.  A pattern seen before launches
+    // nothing; a new one takes the next slot that the current call does not
+    // use.  Slots are rewritten only by later work on this workspace's stream,
+    // so every decode enqueued earlier has read its slot by then.
+    struct El8Key {
+        uint32_t e[8];
+        bool operator==(const El8Key& o) const { return std::memcmp(e, o.e, sizeof(e)) == 0; }
+    };
+    struct El8Hash {
+        size_t operator()(const El8Key& k) const {
+            uint64_t h = 1469598103934665603ull;
+            for (uint32_t v : k.e) h = (h ^ v) * 1099511628211ull;
+            return size_t(h);
+        }
+    };
+    static constexpr unsigned kEl8Slots = 512;
+    uint32_t* el8 = nullptr;
+    std::unordered_map<El8Key, unsigned, El8Hash> el8_map;
+    std::vector<El8Key> el8_key;     // pattern of each slot
+    std::vector<uint64_t> el8_stamp;  // the call that last used each slot
+    std::vector<uint8_t> el8_valid;
+    uint64_t el8_call = 0;
+    unsigned el8_next = 0;
 
     ~Workspace() { release(); }
     // Waits for the work that may still use this workspace, then frees it.
@@ -234,7 +278,12 @@ struct Workspace {
             if (sl.done) (void)hipEventDestroy(sl.done);
             sl = StageSlot{};
         }
-        release_device_memory(dev, {dbuf, dec16, ring_dev, direct});
+        release_device_memory(dev, {dbuf, dec16, ring_dev, direct, el8});
+        el8 = nullptr;
+        el8_map.clear();
+        el8_key.clear();
+        el8_stamp.clear();
+        el8_valid.clear();
         if (ring_host) (void)hipHostFree(ring_host);
         for (int s = 0; s < 2; ++s) {
             if (pipe_stream[s]) (void)hipStreamDestroy(pipe_stream[s]);
@@ -274,7 +323,7 @@ struct Workspace {
             slot_bytes = 0;
         }
         const size_t want = (bytes_per_slot + 4095) / 4096 * 4096;
-        HIP_OK(hipMallocAsync(reinterpret_cast<void**>(&ring_dev), 2 * want, pipe_stream[0]), "allocate device ring");
+        HIP_OK(pool_alloc(reinterpret_cast<void**>(&ring_dev), 2 * want, dev, pipe_stream[0]), "allocate device ring");
         // both pipe streams use it: the second one waits for the allocation
         HIP_OK(hipEventRecord(in_done[0], pipe_stream[0]), "record ring allocation");
         HIP_OK(hipStreamWaitEvent(pipe_stream[1], in_done[0], 0), "order ring allocation");
@@ -292,9 +341,58 @@ struct Workspace {
         if (dbuf) HIP_OK(hipFreeAsync(dbuf, stream), "free scratch");
         dbuf = nullptr;
         dsize = 0;
-        HIP_OK(hipMallocAsync(reinterpret_cast<void**>(&dbuf), want, stream), "allocate scratch");
+        HIP_OK(pool_alloc(reinterpret_cast<void**>(&dbuf), want, dev, stream), "allocate scratch");
         dsize = want;
         return Leopard_Success;
+    }
+    // Starts a call's use of the error-locator cache (slots it takes stay put until the next call).
+    void el8_begin() { ++el8_call; }
+    // The device error locator of erasure bitmap `erased` (8 words): a cached
+    // slot, or a new slot whose computation is appended to `jobs` (flush_el8
+    // launches them, ahead of the decode kernels).
+    LeopardResult el8_slot(const uint32_t* erased, std::vector<El8Job>& jobs, const uint32_t** out) {
+        touched = true;
+        if (!el8) {
+            HIP_OK(pool_alloc(reinterpret_cast<void**>(&el8), size_t(kEl8Slots) * 256, dev, stream),
+                   "allocate error locators");
+            el8_key.assign(kEl8Slots, El8Key{});
+            el8_stamp.assign(kEl8Slots, 0);
+            el8_valid.assign(kEl8Slots, 0);
+        }
+        El8Key k;
+        std::memcpy(k.e, erased, sizeof(k.e));
+        unsigned slot;
+        const auto it = el8_map.find(k);
+        if (it != el8_map.end()) {
+            slot = it->second;
+        } else {
+            unsigned tries = 0;
+            while (el8_stamp[el8_next] == el8_call && tries++ < kEl8Slots) el8_next = (el8_next + 1) % kEl8Slots;
+            if (tries > kEl8Slots) {  // callers split their work into <= kEl8Slots patterns per call
+                tls.last_error = "too many erasure patterns in one call";
+                return Leopard_InvalidInput;
+            }
+            slot = el8_next;
+            el8_next = (el8_next + 1) % kEl8Slots;
+            if (el8_valid[slot]) el8_map.erase(el8_key[slot]);
+            el8_key[slot] = k;
+            el8_valid[slot] = 1;
+            el8_map.emplace(k, slot);
+            El8Job j;
+            std::memcpy(j.erased, erased, sizeof(j.erased));
+            j.slot = slot;
+            jobs.push_back(j);
+        }
+        el8_stamp[slot] = el8_call;
+        *out = el8 + size_t(slot) * 64;
+        return Leopard_Success;
+    }
+    // A slot whose computation failed to launch holds nothing valid.
+    void el8_forget(unsigned slot) {
+        if (slot < el8_valid.size() && el8_valid[slot]) {
+            el8_map.erase(el8_key[slot]);
+            el8_valid[slot] = 0;
+        }
     }
     // Device rows for run_host_direct, stream-ordered like the arena.
     LeopardResult reserve_direct(size_t bytes) {
@@ -303,7 +401,7 @@ struct Workspace {
         if (direct) HIP_OK(hipFreeAsync(direct, stream), "free direct rows");
         direct = nullptr;
         direct_size = 0;
-        HIP_OK(hipMallocAsync(reinterpret_cast<void**>(&direct), bytes, stream), "allocate direct rows");
+        HIP_OK(pool_alloc(reinterpret_cast<void**>(&direct), bytes, dev, stream), "allocate direct rows");
         direct_size = bytes;
         return Leopard_Success;
     }
@@ -677,7 +775,7 @@ void erasures8(unsigned K, unsigned R, unsigned m, const void* const* orig, cons
 // positions, every output in the high half; k_ff8_dec_half), the split decoder
 // when some do (k_ff8_dec_split); otherwise the general n-point decoder.
 int fill_dec8(Ff8DecArgs& a, const DeviceTables* t, unsigned K, unsigned R, const void* const* orig,
-              const void* const* rec, void** work, uint64_t off, uint64_t bytes) {
+              const void* const* rec, void** work, uint64_t off, uint64_t bytes, const uint32_t* el) {
     const unsigned m = next_pow2(R);
     const unsigned Tn = log2u(next_pow2(m + K));
     std::memset(&a, 0, sizeof(a));
@@ -713,8 +811,7 @@ int fill_dec8(Ff8DecArgs& a, const DeviceTables* t, unsigned K, unsigned R, cons
     }
     std::memcpy(a.present, pc.present, sizeof(a.present));
     std::memcpy(a.needed, pc.needed, sizeof(a.needed));
-    std::memcpy(a.erased, erased, sizeof(a.erased));  // the kernels compute the error locator from it
-    a.walsh = t->walsh8;
+    a.el = el;  // this pattern's error locator (k_el8, cached per workspace)
     a.sktab = t->sktab8;
     a.tabs = t->tab8;
     a.K = K;
@@ -733,6 +830,27 @@ int fill_dec8(Ff8DecArgs& a, const DeviceTables* t, unsigned K, unsigned R, cons
     for (unsigned i = 0; i < R && all_rec; ++i) all_rec = rec[i] != nullptr;
     a.dense = all_rec ? 1u : 0u;
     return all_rec ? kDec8HalfDense : kDec8Half;
+}
+
+// Launches the queued error-locator computations (k_el8, kEl8Jobs patterns a launch).
+LeopardResult flush_el8(Workspace& ws, const DeviceTables* t, std::vector<El8Job>& jobs, hipStream_t s) {
+    for (size_t i = 0; i < jobs.size(); i += kEl8Jobs) {
+        El8Args a;
+        std::memset(&a, 0, sizeof(a));
+        const unsigned n = unsigned(std::min<size_t>(kEl8Jobs, jobs.size() - i));
+        std::memcpy(a.job, jobs.data() + i, n * sizeof(El8Job));
+        a.walsh = t->walsh8;
+        a.out = ws.el8;
+        const hipError_t e = launch_error_locator8(a, n, s);
+        if (e != hipSuccess) {
+            for (const El8Job& j : jobs) ws.el8_forget(j.slot);
+            jobs.clear();
+            set_error("error locator kernel", e);
+            return Leopard_Platform;
+        }
+    }
+    jobs.clear();
+    return Leopard_Success;
 }
 
 // LEO_AMD_FF8_INVERT=0 turns the inverse full-loss decoder off (A/B); read once.
@@ -775,9 +893,19 @@ LeopardResult decode_device8(Call& c, uint64_t bytes, uint64_t off, unsigned K, 
         }
         return Leopard_Success;
     }
+    // the error locator of this pattern (computed on the device once per pattern)
+    uint32_t erased[8];
+    erasures8(K, R, next_pow2(R), orig, rec, erased);
+    c.ws->el8_begin();
+    std::vector<El8Job> jobs;
+    const uint32_t* el = nullptr;
+    LeopardResult r = c.ws->el8_slot(erased, jobs, &el);
+    if (r != Leopard_Success) return r;
+    if ((r = flush_el8(*c.ws, c.t, jobs, c.s)) != Leopard_Success) return r;
     Ff8DecArgs a;
     for (uint64_t pos = 0; pos < bytes; pos += kFf8MaxLaunchBytes) {  // see encode_device
-        const int mode = fill_dec8(a, c.t, K, R, orig, rec, work, off + pos, std::min(kFf8MaxLaunchBytes, bytes - pos));
+        const int mode =
+            fill_dec8(a, c.t, K, R, orig, rec, work, off + pos, std::min(kFf8MaxLaunchBytes, bytes - pos), el);
         HIP_OK(mode == kDec8General ? launch_ff8_decode(Tn, a, c.s)
                : mode == kDec8Split ? launch_ff8_decode_split(Tn - 1, a, c.s)
                                     : launch_ff8_decode_half(Tn - 1, a, c.s),
@@ -832,7 +960,8 @@ LeopardResult decode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
     const size_t dec16_bytes = off_rl + 65536 * 4;
     Workspace& ws = *c.ws;
     ws.touched = true;
-    if (!ws.dec16) HIP_OK(hipMallocAsync(reinterpret_cast<void**>(&ws.dec16), dec16_bytes, c.s), "allocate decoder state");
+    if (!ws.dec16)
+        HIP_OK(pool_alloc(reinterpret_cast<void**>(&ws.dec16), dec16_bytes, ws.dev, c.s), "allocate decoder state");
     std::vector<uint32_t> key(2 + bitmap_words, 0);
     key[0] = K;
     key[1] = R;
@@ -1085,6 +1214,7 @@ int pipe_mode() {
 struct HostRun {
     uint64_t first, count, stride;
 };
+constexpr uint64_t kRunMaxGap = 1ull << 20;  // bytes between two rows of one run
 template <class P>
 std::vector<HostRun> host_runs(const std::vector<P>& v, uint64_t bytes) {
     std::vector<HostRun> runs;
@@ -1095,7 +1225,10 @@ std::vector<HostRun> host_runs(const std::vector<P>& v, uint64_t bytes) {
             const uint8_t* cur = v[i];
             if (cur > prev) {
                 const uint64_t d = uint64_t(cur - prev);
-                if (d >= bytes && (b.count == 1 ? true : d == b.stride)) {
+                // a run's first pair sets its stride: only pitches that leave a
+                // small gap (rows of one array, or of a wider one) start a run,
+                // never two unrelated allocations far apart
+                if (d >= bytes && (b.count == 1 ? d - bytes <= kRunMaxGap : d == b.stride)) {
                     b.stride = d;
                     ++b.count;
                     continue;
@@ -1108,6 +1241,7 @@ std::vector<HostRun> host_runs(const std::vector<P>& v, uint64_t bytes) {
 }
 constexpr size_t kDirectMaxRuns = 16;                 // more runs: the gather / scatter ring
 constexpr uint64_t kDirectMaxBytes = 8ull << 30;      // device rows of one direct call
+constexpr uint64_t kDirectKeepBytes = 256ull << 20;   // direct rows kept for the next call (larger: freed)
 
 // Host pieces that form a few row runs (the usual caller layout: pieces are
 // rows of one or a few arrays) go straight between the caller's pageable
@@ -1125,7 +1259,11 @@ LeopardResult run_host_direct(Call& c, uint64_t bytes, const std::vector<const u
     if (rin.size() + rout.size() > kDirectMaxRuns) return Leopard_Success;
     Workspace& ws = *c.ws;
     LeopardResult r = ws.reserve_direct(rows * bytes);
-    if (r != Leopard_Success) return r;
+    if (r != Leopard_Success) {  // no room for the rows: the ring (bounded slots) does the call
+        (void)hipGetLastError();
+        tls.last_error.clear();
+        return Leopard_Success;
+    }
     uint8_t* din = ws.direct;
     uint8_t* dout = ws.direct + nin * bytes;
     for (const HostRun& run : rin) {
@@ -1145,6 +1283,11 @@ LeopardResult run_host_direct(Call& c, uint64_t bytes, const std::vector<const u
         else
             HIP_OK(hipMemcpy2DAsync(hout[run.first], run.stride, src, bytes, bytes, run.count, hipMemcpyDeviceToHost, c.s),
                    "download rows");
+    }
+    if (ws.direct_size > kDirectKeepBytes) {  // large rows do not stay with the thread: freed after this call's copies
+        HIP_OK(hipFreeAsync(ws.direct, c.s), "free direct rows");
+        ws.direct = nullptr;
+        ws.direct_size = 0;
     }
     *done = true;
     return Leopard_Success;
@@ -1714,12 +1857,14 @@ bool run_slab_batch8(int dev, RangeCache& rc, unsigned count, uint64_t bytes, un
     return true;
 }
 
-template <class Args, class Fill, class Launch>
-LeopardResult run_batch8(int dev, unsigned count, Fill fill, Launch launch) {
+// prep(c): work enqueued on the call's stream ahead of the batch kernel.
+template <class Args, class Fill, class Launch, class Prep>
+LeopardResult run_batch8(int dev, unsigned count, Fill fill, Launch launch, Prep prep) {
     DeviceGuard guard(dev);
     Call c;
     LeopardResult r = begin_call(dev, c);
     if (r != Leopard_Success) return r;
+    if ((r = prep(c)) != Leopard_Success) return r;
     const size_t bytes = size_t(count) * sizeof(Args);
     r = c.ws->reserve_device(bytes);
     if (r != Leopard_Success) return r;
@@ -1733,13 +1878,21 @@ LeopardResult run_batch8(int dev, unsigned count, Fill fill, Launch launch) {
     HIP_OK(launch(dargs, kind, c.s), "batch kernel");
     return finish(c, false);
 }
+template <class Args, class Fill, class Launch>
+LeopardResult run_batch8(int dev, unsigned count, Fill fill, Launch launch) {
+    return run_batch8<Args>(dev, count, fill, launch, [](Call&) { return Leopard_Success; });
+}
+// objects (erasure patterns: one error-locator slot each) per batched GF(2^8) decode launch
+constexpr unsigned kDecBatchChunk = Workspace::kEl8Slots / 2;
 
 LeopardResult encode_batch(unsigned count, uint64_t bytes, unsigned K, unsigned R, unsigned work_count,
                            const void* const* const* orig, void** const* work) {
     if (!orig || !work) return Leopard_InvalidInput;
     for (unsigned o = 0; o < count; ++o) {
-        const LeopardResult r = check_encode(bytes, K, R, work_count, orig[o], work[o]);
+        LeopardResult r = check_encode(bytes, K, R, work_count, orig[o], work[o]);
         if (r != Leopard_Success) return r;
+        // every recovery piece is written (the one-launch path stores through each)
+        if ((r = missing_output(work[o], R, nullptr)) != Leopard_Success) return r;
     }
     if (count == 0) return Leopard_Success;
     const unsigned m = next_pow2(R), n = next_pow2(m + K);
@@ -1827,16 +1980,34 @@ LeopardResult decode_batch(unsigned count, uint64_t bytes, unsigned K, unsigned 
                 [&](const Ff8EncArgs* d, int, hipStream_t s) {
                     return launch_ff8_encode_batch(Tn - 1, d, count, uint32_t(bytes / 4), false, kFormDenseDec, s);
                 });
-        if (on_dev)
-            return run_batch8<Ff8DecArgs>(
-                dev, count,
-                [&](Ff8DecArgs& a, const DeviceTables* t, unsigned o) {
-                    return fill_dec8(a, t, K, R, orig[o], rec[o], work[o], 0, bytes);
-                },
-                [&](const Ff8DecArgs* d, int mode, hipStream_t s) {
-                    return launch_ff8_decode_batch(mode != kDec8General ? Tn - 1 : Tn, d, count, uint32_t(bytes / 4),
-                                                   mode, s);
-                });
+        if (on_dev) {
+            for (unsigned o0 = 0; o0 < count; o0 += kDecBatchChunk) {
+                const unsigned nb = std::min(kDecBatchChunk, count - o0);
+                std::vector<const uint32_t*> els(nb);
+                const LeopardResult r = run_batch8<Ff8DecArgs>(
+                    dev, nb,
+                    [&](Ff8DecArgs& a, const DeviceTables* t, unsigned o) {
+                        return fill_dec8(a, t, K, R, orig[o0 + o], rec[o0 + o], work[o0 + o], 0, bytes, els[o]);
+                    },
+                    [&](const Ff8DecArgs* d, int mode, hipStream_t s) {
+                        return launch_ff8_decode_batch(mode != kDec8General ? Tn - 1 : Tn, d, nb, uint32_t(bytes / 4),
+                                                       mode, s);
+                    },
+                    [&](Call& c) -> LeopardResult {  // the error locators of the new patterns, one launch
+                        c.ws->el8_begin();
+                        std::vector<El8Job> jobs;
+                        for (unsigned o = 0; o < nb; ++o) {
+                            uint32_t erased[8];
+                            erasures8(K, R, m, orig[o0 + o], rec[o0 + o], erased);
+                            const LeopardResult re = c.ws->el8_slot(erased, jobs, &els[o]);
+                            if (re != Leopard_Success) return re;
+                        }
+                        return flush_el8(*c.ws, c.t, jobs, c.s);
+                    });
+                if (r != Leopard_Success) return r;
+            }
+            return Leopard_Success;
+        }
     }
     for (unsigned o = 0; o < count; ++o) {
         const LeopardResult r = decode_any(bytes, 0, K, R, orig[o], rec[o], work[o]);

@@ -103,8 +103,7 @@ struct Ff8DecArgs {
     uint64_t ptr[kFf8Ptrs];        // position p: received piece / output of a lost original / 0
     uint32_t present[kPyr8Words];  // pyramid of received positions (Pyr8Live)
     uint32_t needed[kPyr8Words];   // pyramid of lost originals
-    uint32_t erased[kFf8Ptrs / 32]; // erasure bitmap over the 256 positions (LeopardFF8.cpp:1825-1840)
-    const uint32_t* walsh;         // LogWalsh (256 entries): the kernels compute the error locator
+    const uint32_t* el;            // error locator of this pattern, one byte per position (k_el8's output)
     const uint32_t* sktab;
     const uint32_t* tabs;          // multiply tables by log value; entry 256 is all zero
     const uint32_t* fused;         // k_ff8_dec_half: fused top-layer table of this m (= encoder chunk 0's)
@@ -113,11 +112,24 @@ struct Ff8DecArgs {
     uint32_t dense;                // half decoder with K = R = m, every recovery received (host-side dispatch)
     __host__ __device__ uint64_t piece(unsigned i) const { return ptr[i]; }
 };
+// GF(2^8) error locators of up to kEl8Jobs erasure patterns in one launch
+// (k_el8): job i writes the 256 el bytes of bitmap erased (LeopardFF8.cpp:
+// 1825-1840) to out + 64 * slot dwords.
+constexpr unsigned kEl8Jobs = 64;
+struct El8Job {
+    uint32_t erased[kFf8Ptrs / 32];
+    uint32_t slot;
+};
+struct El8Args {
+    El8Job job[kEl8Jobs];
+    const uint32_t* walsh;  // LogWalsh (256 entries)
+    uint32_t* out;
+};
 // GF(2^8) decoder kinds of one argument block (fill_dec8, launch_ff8_decode_batch)
 // (ordered from the least specialised: a batch runs the minimum over its objects;
 // the split decoder also handles the half kinds, with no high-half input)
 constexpr int kDec8General = 0, kDec8Split = 1, kDec8Half = 2, kDec8HalfDense = 3;
-// LDS dwords of the in-kernel GF(2^8) error locator (one byte per position)
+// LDS dwords of the GF(2^8) error locator in the decode kernels (one byte per position)
 constexpr size_t kEl8Dwords = kFf8Ptrs / 4;
 // Forms of the GF(2^8) encoder tile (k_ff8_enc): general (pruned, chunked),
 // dense encode (one chunk, K = R = m), dense inverse (full-loss decode of a
@@ -157,6 +169,7 @@ hipError_t launch_decode16_small_lo(const DecArgs& a, hipStream_t s);
 hipError_t launch_decode16_small_fin(const DecArgs& a, hipStream_t s);
 hipError_t launch_ff8_encode(unsigned T, const Ff8EncArgs& a, hipStream_t s);
 hipError_t launch_ff8_decode(unsigned T, const Ff8DecArgs& a, hipStream_t s);
+hipError_t launch_error_locator8(const El8Args& a, unsigned count, hipStream_t s);
 // Batched GF(2^8) launches: `count` argument blocks in device memory (same T,
 // column count and chunk structure), one grid (strips x objects).  For the
 // decoder, mode = the least specialised kDec8* kind over the objects (T is the

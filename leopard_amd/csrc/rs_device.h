@@ -29,7 +29,7 @@
 // separate libraries with them; the shipped library has LAMD_ABLATE == 0):
 // 1 = no butterfly arithmetic, 2 = no LDS transposes, 4 = no piece loads,
 // 8 = no piece stores, 16 = fused kernels return at once (launch floor),
-// 32 = FF8 decoder: no in-kernel error locator, 64 = no formal derivative,
+// 32 = (unused), 64 = no formal derivative,
 // 128 = FF8 decoder: no scale / reveal multiplies, 256 = no table staging.
 #ifndef LAMD_ABLATE
 #define LAMD_ABLATE 0

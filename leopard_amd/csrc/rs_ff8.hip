@@ -388,18 +388,27 @@ __global__ void __launch_bounds__(threads_for(T, RB), LAMD_SLAB_WAVES) k_ff8_enc
 
 // Error locator of the decoders (LeopardFF8.cpp:1845-1853, FWHT :80-130):
 //   el = FWHT( LogWalsh * FWHT(erasures) )  mod 255,
-// a 256-point Walsh-Hadamard transform mod 255, twice.  Wave 0 of every
-// workgroup computes it in the prologue, while the other waves wait for their
-// piece loads: 4 positions a lane (p = lane + 64 j), six layers across lanes
-// (__shfl_xor) and two in registers.  Fully reduced mod 255 (the reference
-// reduces partially, 255 standing for 0: the same residues; the multiply tables
-// of log 0 and log 255 are the same, x * exp(0) = x * exp(255)).  The result
-// lands in LDS, one byte per position.
+// a 256-point Walsh-Hadamard transform mod 255, twice.  k_el8 computes it once
+// per erasure pattern (the host caches the result per workspace, keyed by the
+// pattern: a repeated pattern launches nothing), one wave per pattern, 4
+// positions a lane (p = 4 lane + j: one dword of el bytes per lane), six
+// layers across lanes (__shfl_xor) and two in registers.  Fully reduced mod 255
+// (the reference reduces partially, 255 standing for 0: the same residues; the
+// multiply tables of log 0 and log 255 are the same, x * exp(0) = x * exp(255)).
+// The decode kernels then copy the 256 el bytes into LDS in their prologue
+// (ElLoad8): one dword load per lane of wave 0, issued ahead of the piece loads.
 struct Mod8 {
     LDEV static unsigned add(unsigned a, unsigned b) { const unsigned s = a + b; return s >= 255u ? s - 255u : s; }
     LDEV static unsigned sub(unsigned a, unsigned b) { const unsigned s = a + 255u - b; return s >= 255u ? s - 255u : s; }
 };
+// FWHT_2 {a, b} = {a + b, a - b}: position bits 0, 1 in registers, bits 2..7 = lane bits 0..5
 LDEV void fwht256_mod255(unsigned (&e)[4], unsigned lane) {
+    const unsigned a0 = Mod8::add(e[0], e[1]), a1 = Mod8::sub(e[0], e[1]);
+    const unsigned a2 = Mod8::add(e[2], e[3]), a3 = Mod8::sub(e[2], e[3]);
+    e[0] = Mod8::add(a0, a2);
+    e[2] = Mod8::sub(a0, a2);
+    e[1] = Mod8::add(a1, a3);
+    e[3] = Mod8::sub(a1, a3);
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1)
 #pragma unroll
@@ -407,39 +416,31 @@ LDEV void fwht256_mod255(unsigned (&e)[4], unsigned lane) {
             const unsigned o = unsigned(__shfl_xor(int(e[j]), d));
             e[j] = (lane & d) ? Mod8::sub(o, e[j]) : Mod8::add(e[j], o);
         }
-    const unsigned a0 = Mod8::add(e[0], e[1]), a1 = Mod8::sub(e[0], e[1]);
-    const unsigned a2 = Mod8::add(e[2], e[3]), a3 = Mod8::sub(e[2], e[3]);
-    e[0] = Mod8::add(a0, a2);
-    e[2] = Mod8::sub(a0, a2);
-    e[1] = Mod8::add(a1, a3);
-    e[3] = Mod8::sub(a1, a3);
 }
-// load(): the LogWalsh entries of wave 0's positions, issued at kernel start,
-// ahead of the piece loads (vmcnt retires in order: waiting for these then does
-// not wait for the pieces); run(): the two transforms, then el -> LDS.
-struct ErrorLocator8 {
-    unsigned w[4];
-    LDEV void load(const Ff8DecArgs& a, unsigned wave, unsigned lane) {
-        if (wave != 0) return;
+__global__ void __launch_bounds__(64) k_el8(El8Args a) {
+    const El8Job& job = a.job[blockIdx.x];
+    const unsigned lane = threadIdx.x;
+    const uint32_t ebits = (job.erased[lane >> 3] >> ((lane & 7) * 4)) & 0xFu;  // positions 4 lane .. 4 lane + 3
+    unsigned e[4], w[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) w[j] = a.walsh[lane + 64u * j];
+    for (int j = 0; j < 4; ++j) {
+        w[j] = a.walsh[4 * lane + j];
+        e[j] = (ebits >> j) & 1u;
     }
-    LDEV void run(const Ff8DecArgs& a, uint8_t* el, unsigned wave, unsigned lane) {
-        if (wave != 0) return;
-        unsigned e[4];
+    fwht256_mod255(e, lane);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const unsigned p = lane + 64u * j;
-            e[j] = (cload(a.erased + (p >> 5)) >> (p & 31)) & 1u;
-        }
-        if constexpr ((LAMD_ABLATE & 32) == 0) {
-            fwht256_mod255(e, lane);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) e[j] = (e[j] * w[j]) % 255u;
-            fwht256_mod255(e, lane);
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) el[lane + 64u * j] = uint8_t(e[j]);
+    for (int j = 0; j < 4; ++j) e[j] = (e[j] * w[j]) % 255u;
+    fwht256_mod255(e, lane);
+    a.out[size_t(job.slot) * 64 + lane] = e[0] | (e[1] << 8) | (e[2] << 16) | (e[3] << 24);
+}
+// The error locator of this launch's pattern (k_el8's output) into LDS.
+struct ElLoad8 {
+    uint32_t v;
+    LDEV void load(const Ff8DecArgs& a, unsigned wave, unsigned lane) {
+        if (wave == 0) v = *gptr<const uint32_t>(a.el + lane);
+    }
+    LDEV void store(uint8_t* el, unsigned wave, unsigned lane) const {
+        if (wave == 0) reinterpret_cast<uint32_t*>(el)[lane] = v;
     }
 };
 
@@ -475,7 +476,7 @@ LDEV void ff8_dec(const Ff8DecArgs& a) {
     sk_stage.load(a.sktab);
     log_stage.load(a.tabs);
     const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    ErrorLocator8 elc;
+    ElLoad8 elc;
     elc.load(a, w, lane);
     const Cols cl = strip_cols(a.nunits, lane);
     const PieceSpace ps{0, 0, 0};
@@ -491,7 +492,7 @@ LDEV void ff8_dec(const Ff8DecArgs& a) {
         for (int r = 0; r < TL::NR; ++r) v[r][0] = present(pos(r), 0) ? gload(pp[r], cl) : 0u;
     }
     STAMP(1);
-    elc.run(a, el, w, lane);
+    elc.store(el, w, lane);
     sk_stage.store(sk);
     log_stage.store(ltab);
     __syncthreads();
@@ -566,7 +567,7 @@ LDEV void ff8_dec_half(const Ff8DecArgs& a) {
     sk_stage.load(a.sktab);
     log_stage.load(a.tabs);
     const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    ErrorLocator8 elc;
+    ElLoad8 elc;
     elc.load(a, w, lane);
     const Cols cl = strip_cols(a.nunits, lane);
     const PieceSpace low{0, 0, 0}, high{0, 0, m};
@@ -584,7 +585,7 @@ LDEV void ff8_dec_half(const Ff8DecArgs& a) {
 #pragma unroll
         for (int r = 0; r < TL::NR; ++r) v[r][0] = present(lpos(r), 0) ? gload(pp[r], cl) : 0u;
     }
-    elc.run(a, el, w, lane);
+    elc.store(el, w, lane);
     sk_stage.store(sk);
     log_stage.store(ltab);
     __syncthreads();
@@ -642,7 +643,7 @@ LDEV void ff8_dec_split(const Ff8DecArgs& a) {
     sk_stage.load(a.sktab);
     log_stage.load(a.tabs);
     const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    ErrorLocator8 elc;
+    ElLoad8 elc;
     elc.load(a, w, lane);
     const Cols cl = strip_cols(a.nunits, lane);
     const PieceSpace low{0, 0, 0}, high{0, 0, m};
@@ -659,7 +660,7 @@ LDEV void ff8_dec_split(const Ff8DecArgs& a) {
 #pragma unroll
         for (int r = 0; r < TL::NR; ++r) x[r][0] = present(lpos(r), 0) ? gload(pp[r], cl) : 0u;
     }
-    elc.run(a, el, w, lane);
+    elc.store(el, w, lane);
     sk_stage.store(sk);
     log_stage.store(ltab);
     __syncthreads();
@@ -851,6 +852,12 @@ extern "C" __attribute__((visibility("default"))) int leo_amd_debug_stamps(void*
     return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &buf, sizeof(buf)) == hipSuccess ? 0 : -1;
 }
 #endif
+
+hipError_t launch_error_locator8(const El8Args& a, unsigned count, hipStream_t s) {
+    if (count == 0 || count > kEl8Jobs) return hipErrorInvalidValue;
+    void* params[] = {const_cast<El8Args*>(&a)};
+    return hipLaunchKernel(reinterpret_cast<const void*>(&k_el8), dim3(count), dim3(64), params, 0, s);
+}
 
 hipError_t launch_ff8_encode(unsigned T, const Ff8EncArgs& a, hipStream_t s) {
     hipError_t e = hipErrorInvalidValue;

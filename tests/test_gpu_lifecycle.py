@@ -333,3 +333,51 @@ def test_two_rank_processes_share_the_gpu_sliced(leo):
     assert sha(shared["rec_1000"]) == dig["hash_digests"]["1000_200_65536"]
     assert sha(shared["dec_1000"]) == dig["decode_hash_digests"]["1000_200_65536"]
     assert sha(shared["rec_32768"]) == dig["hash_digests"]["32768_32768_65536"]
+
+
+_TUNED_SCRIPT = r"""
+import sys, numpy as np
+sys.path.insert(0, {repo!r}); sys.path.insert(0, {tests!r})
+import leopard_amd as leo, oracle_lib as ol, torch
+assert leo.leo_init() == 0, leo.last_error()
+o = ol.oracle()
+# GF(2^16) multi-pass (m = 1024, n = 4096): LEO_AMD_SLICE_MB=1 cuts 4096-byte columns into 512-byte slices
+k, r, b = 2000, 1000, 4096
+data = ol.pcg_bytes(11, k, k, b)
+dev = torch.from_numpy(data).cuda()
+rec = leo.encode(dev, r)
+torch.cuda.synchronize()
+exp = o.encode(data, r)
+assert np.array_equal(rec.cpu().numpy(), exp), "sliced encode"
+lost = list(range(0, k, 3))[:r]
+got = leo.decode(dev, rec, lost, [])
+torch.cuda.synchronize()
+assert all(torch.equal(got[i], dev[i]) for i in lost), "sliced decode"
+# host ring with LEO_AMD_SLOT_MB=1: scattered pageable pieces, many slices
+k, r, b = 128, 64, 65536
+data = ol.pcg_bytes(12, k, k, b)
+din = [np.zeros(b, dtype=np.uint8) for _ in range(k)]
+din.sort(key=lambda x: -x.ctypes.data)  # descending addresses: no row runs, so the ring takes the call
+for i in range(k):
+    din[i][:] = data[i]
+wc = leo.leo_encode_work_count(k, r)
+work = [np.zeros(b, dtype=np.uint8) for _ in range(wc)]
+work.sort(key=lambda x: -x.ctypes.data)
+assert leo.leo_encode(b, k, r, wc, [x.ctypes.data for x in din], [x.ctypes.data for x in work]) == 0, leo.last_error()
+assert np.array_equal(np.stack(work[:r]), o.encode(data, r)), "ring encode"
+print("tuned ok")
+"""
+
+
+def test_tuning_switches_at_non_default_values():
+    """LEO_AMD_SLICE_MB (device scratch per GF(2^16) multi-pass slice) and
+    LEO_AMD_SLOT_MB (host ring slot) at small non-default values: many column
+    slices, results equal to the oracle.  Read once per process, so they run in
+    a child process with the variables set."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, LEO_AMD_SLICE_MB="1", LEO_AMD_SLOT_MB="1")
+    code = _TUNED_SCRIPT.format(repo=os.path.dirname(here), tests=here)
+    p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0 and "tuned ok" in p.stdout, (p.stdout[-2000:], p.stderr[-3000:])

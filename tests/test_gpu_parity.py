@@ -396,13 +396,16 @@ def test_host_pipeline_roundtrip(leo, k, r, b, loss):
 
 @pytest.mark.parametrize("k,r,b,layout", [(128, 128, 1 << 16, "strided"), (128, 128, 1 << 16, "scattered"),
                                           (1000, 200, 4096, "strided"), (1000, 200, 4096, "scattered"),
-                                          (200, 55, 64 * 100, "two_arrays")])
+                                          (200, 55, 64 * 100, "two_arrays"), (128, 128, 1 << 16, "ascending"),
+                                          (100, 20, 640, "ascending")])
 def test_host_layouts_direct_and_ring(leo, k, r, b, layout):
     """The two host-memory paths: pieces forming a few row runs go by direct
     SDMA copies (1-D for dense rows, 2-D for rows of a wider array:
     "strided", "two_arrays"), pieces at scattered addresses through the
     gather / scatter ring ("scattered": one allocation per piece, handed over
-    in descending address order, so no two form a run).  Encode must match the
+    in descending address order, so no two form a run; "ascending": the same
+    allocations in ascending order, where neighbours at a small gap form 2-D
+    runs and larger gaps start new runs).  Encode must match the
     oracle and the decode of every lost original must rebuild it."""
     data = ol.pcg_bytes(8, k, k, b)
     wc, dwc = leo.leo_encode_work_count(k, r), leo.leo_decode_work_count(k, r)
@@ -415,6 +418,9 @@ def test_host_layouts_direct_and_ring(leo, k, r, b, layout):
             h = n // 2
             a1, a2 = np.zeros((h, b), dtype=np.uint8), np.zeros((n - h, b), dtype=np.uint8)
             v = [a1[i] for i in range(h)] + [a2[i] for i in range(n - h)]
+        elif layout == "ascending":  # separate allocations in ascending address order: runs only over small gaps
+            v = [np.zeros(b, dtype=np.uint8) for _ in range(n)]
+            v.sort(key=lambda x: x.ctypes.data)
         else:
             v = [np.zeros(b, dtype=np.uint8) for _ in range(n)]
             v.sort(key=lambda x: -x.ctypes.data)  # descending addresses: never a run
@@ -617,6 +623,11 @@ def test_batch_full_loss_and_validation(leo):
     pr_bad[2] = [None] * r  # object 2 received nothing
     assert leo.leo_amd_decode_batch(b, k, r, dwc, short, pr_bad, pd) == R.NeedMoreData
     assert leo.leo_amd_encode_batch(b, k, r, wc, [], []) == R.Success
+    # a NULL recovery destination is rejected before anything runs (a single
+    # leo_encode returns the same), never written through
+    pw_bad = [list(x) for x in pw]
+    pw_bad[1][5] = None
+    assert leo.leo_amd_encode_batch(b, k, r, wc, po, pw_bad) == R.InvalidInput
 
 
 @pytest.mark.parametrize("k,r,b,loss", [(128, 128, 1 << 16, 128), (100, 30, 64 * 1000, 17), (1000, 200, 1 << 13, 200),

@@ -84,6 +84,8 @@ def _load():
         "leo_amd_last_error": (ctypes.c_char_p, []),
     }
     for name, (res, args) in sig.items():
+        if os.environ.get("LEOPARD_AMD_LIB") and not hasattr(lib, name):
+            continue  # an older experiment build (tools/ A/B runs) may lack later extensions
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

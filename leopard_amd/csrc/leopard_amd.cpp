@@ -570,6 +570,7 @@ struct MapBuilder {
 // Pieces of at most this many bytes count as narrow columns for the small
 // GF(2^16) kernels (rs_ff16_small.hip): 256 KiB = 2048 strips of 128 bytes.
 constexpr uint64_t kNarrowColumnsMax = 256 << 10;
+constexpr uint64_t kOnePassMinBytes = 32 << 10;
 
 // Columns per GF(2^8) launch: its argument block counts dword columns in 32 bits.
 constexpr uint64_t kFf8MaxLaunchBytes = 1ull << 32;
@@ -972,7 +973,12 @@ LeopardResult decode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
     // (rs_ff16_small.hip), whose only intermediate is U (tiles with received data).
     const unsigned ntiles_in = (m + K + (1u << kLoBits) - 1) >> kLoBits;
     const bool narrow = g_q16_ok && decode16_small_supported(Tn) && bytes <= kNarrowColumnsMax;
-    const uint64_t slab_pieces = narrow ? uint64_t(ntiles_in) << kLoBits : 2ull * n;  // U (+ A, multi-pass)
+    // few output tiles and enough column strips to fill the GPU (>= 32 KiB
+    // pieces: 256 strips): the one-pass form (no U slab); narrower calls keep
+    // the two passes, whose grids also spread over the tiles
+    const bool one_pass = narrow && bytes >= kOnePassMinBytes &&
+                          decode16_one_supported(((m + K - 1) >> kLoBits) - (m >> kLoBits) + 1);
+    const uint64_t slab_pieces = one_pass ? 0 : narrow ? uint64_t(ntiles_in) << kLoBits : 2ull * n;  // U (+ A, multi-pass)
     const uint64_t slice = narrow ? bytes : mall_slice(bytes, slab_pieces);
     const size_t table_bytes = (mb.bytes() + 255) / 256 * 256;
     const size_t off_slab = table_bytes;
@@ -1034,6 +1040,10 @@ LeopardResult decode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
         a.tile0 = m >> kLoBits;
         a.nout = ((m + K - 1) >> kLoBits) - a.tile0 + 1;
         a.nunits = bytes / 8;
+        if (one_pass) {  // no intermediate at all
+            HIP_OK(launch_decode16_one(a, c.s), "decode");
+            return Leopard_Success;
+        }
         a.a_out = a.a_in = PieceMap{nullptr, ws.dbuf + off_slab, bytes, 0};
         HIP_OK(launch_decode16_small_lo(a, c.s), "decode pass 1");
         HIP_OK(launch_decode16_small_fin(a, c.s), "decode pass 2");

@@ -167,6 +167,10 @@ hipError_t launch_encode16_small(unsigned Tm, const EncArgs& a, hipStream_t s);
 bool decode16_small_supported(unsigned Tn);
 hipError_t launch_decode16_small_lo(const DecArgs& a, hipStream_t s);
 hipError_t launch_decode16_small_fin(const DecArgs& a, hipStream_t s);
+// one pass (scale + low IFFT per received tile folded into per-lane Z
+// accumulators, then low FFT + reveal per output tile) when nout is small
+bool decode16_one_supported(unsigned nout);
+hipError_t launch_decode16_one(const DecArgs& a, hipStream_t s);
 hipError_t launch_ff8_encode(unsigned T, const Ff8EncArgs& a, hipStream_t s);
 hipError_t launch_ff8_decode(unsigned T, const Ff8DecArgs& a, hipStream_t s);
 hipError_t launch_error_locator8(const El8Args& a, unsigned count, hipStream_t s);

@@ -46,6 +46,18 @@
 #ifndef LAMD_FF16_INFLIGHT  // GF(2^16) butterflies a wave keeps in flight (scheduling window)
 #define LAMD_FF16_INFLIGHT 2
 #endif
+// 1: every tile exchange and layer takes an opaque copy of the wave index, so
+// the per-lane LDS and table addresses derived from it are computed where they
+// are used instead of being hoisted and kept live across the transform (for
+// kernels whose registers hold more than the tile, e.g. the one-pass decoder's
+// accumulators; rs_ff16_one.hip)
+#ifndef LAMD_TILE_OPAQUE_W
+#define LAMD_TILE_OPAQUE_W 0
+#endif
+#define LAMD_OPAQUE_W(w)                                        \
+    do {                                                        \
+        if constexpr (LAMD_TILE_OPAQUE_W) asm volatile("" : "+v"(w)); \
+    } while (0)
 
 namespace lamd {
 
@@ -683,6 +695,7 @@ struct Tile {
     template <bool kInverse, int LAY, int L, class Win, class Pred>
     LDEV static void layer(Reg& x, unsigned w, const PieceSpace& ps, const Win& win, const Pred& pred) {
         if constexpr ((LAMD_ABLATE & 1) != 0) return;
+        LAMD_OPAQUE_W(w);
         constexpr int rb = L - lo(LAY);
         static_assert(rb >= 0 && rb < R, "layer not in this layout");
         constexpr int half = 1 << rb;
@@ -888,6 +901,7 @@ struct Tile {
     template <int FROM, int TO>
     LDEV static void transpose(Reg& x, unsigned w, unsigned lane, uint32_t* lds) {
         if constexpr ((LAMD_ABLATE & 2) != 0) return;
+        LAMD_OPAQUE_W(w);
         Reg y;
         static_for<0, (1 << S)>([&](auto Q) {
             constexpr unsigned q = decltype(Q)::value;

@@ -447,6 +447,306 @@ __global__ void __launch_bounds__((threads_n<8, R, LW>()), LAMD_DEC16N_FIN_WAVES
     STAMP16(4);
 }
 
+// ------------------------------------------------------- one-pass decode --
+//
+// The same decoder in ONE pass per column strip (no U slab): a workgroup owns
+// a strip of LW units of every position and walks the received tiles t' in
+// order -- scale, low IFFT, and fold the result straight into the Z
+// accumulators of every output tile, which stay in registers for the whole
+// kernel -- then runs the low FFT and the reveal of each output tile:
+//   for each received tile t':   U = IFFT_lo^(t')( el * received tile t' )
+//                                Z_t ^= q[t ^ t'] U   (t != t'),   Z_t ^= D_lo U   (t = t')
+//   for each output tile t:      lost originals of t = FFT_lo^(t)(Z_t) * exp(-el)
+// (LeopardFF16.cpp:1652-1775; the split F (I + D) I = F_lo (Q + D_lo) I_lo as in
+// the two-pass form above).  U is never written to memory: a call reads the
+// received pieces once and writes the lost originals once.  NZ output tiles
+// (tiles holding a lost original, [tile0, tile0 + nout)) are held per lane
+// (NZ * 2^R * 2 dwords); calls with more use the two-pass form.
+//
+// Tables reach LDS by LDS-DMA (global_load_lds_dwordx4: no registers, no
+// per-lane LDS stores): a tile's skew set (the decoder's IFFT and FFT of one
+// tile use the same skew positions, base -1, LeopardFF16.cpp:1737, 1764) and
+// its 256 scale / reveal tables, whose log values the workgroup keeps in LDS.
+// Each tile boundary is one exposed wait (the DMA of the next tables and the
+// next pieces' loads); two workgroups per CU cover each other's.
+
+// 16 bytes per lane from src (per lane) to dst + 16 * lane (dst wave-uniform)
+LDEV void dma16(const uint32_t* src, uint32_t* dst) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src),
+                                     (__attribute__((address_space(3))) void*)(dst), 16, 0, 0);
+#endif
+}
+LDEV void wait_dma() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// 16-byte unit u of a table set laid out by tab16_slot (slot s at 5 s + (s >> 3)
+// + (s >> 6) units): its slot and its unit inside the slot, or slot ~0u for a
+// padding unit.
+LDEV unsigned unit_slot(unsigned u, unsigned& k) {
+    const unsigned b = u / 329u, r = u - b * 329u;
+    const unsigned g = r / 41u, r2 = r - g * 41u;
+    if (r == 328u || r2 == 40u) {
+        k = 0;
+        return ~0u;
+    }
+    const unsigned i = r2 / 5u;
+    k = r2 - i * 5u;
+    return 64u * b + 8u * g + i;
+}
+constexpr unsigned kSetUnits = unsigned(tab16_set_dwords(8) / 4);  // = tab16_slot(256) / 4
+static_assert(tab16_slot(256) / 4 == kSetUnits, "skew and log sets have the same footprint");
+// skew set of tile hi_fixed >> 8 at skew base -1 (Tabs16Stage's entries)
+// (lane is made opaque: the unit -> slot arithmetic is redone at each use
+// instead of being hoisted out of the tile loops and kept live)
+template <int NW>
+LDEV void dma_skew_set(uint32_t* set, const uint32_t* sktab, unsigned hi_fixed, unsigned wave, unsigned lane) {
+    asm volatile("" : "+v"(lane));
+    for (unsigned c = wave; c * 64u < kSetUnits; c += NW) {
+        const unsigned u = c * 64u + lane;
+        unsigned k;
+        unsigned sl = unit_slot(u, k);
+        if (sl == ~0u || sl == 0u) sl = 1u;  // padding and the unused slot 0: any valid entry
+        if (u < kSetUnits) dma16(sktab + size_t(hi_fixed + sl - 1u) * 24u + k * 4u, set + c * 256u);
+    }
+}
+// the multiply tables of log values logs[0, 256) (LDS), slot p = position p
+template <int NW>
+LDEV void dma_log_set(uint32_t* dst, const uint32_t* tabs, const uint32_t* logs, unsigned wave, unsigned lane) {
+    asm volatile("" : "+v"(lane));
+    for (unsigned c = wave; c * 64u < kSetUnits; c += NW) {
+        const unsigned u = c * 64u + lane;
+        unsigned k;
+        unsigned p = unit_slot(u, k);
+        if (p == ~0u) p = 0u;
+        if (u < kSetUnits) dma16(tabs + size_t(logs[p]) * 24u + k * 4u, dst + c * 256u);
+    }
+}
+
+#ifndef LAMD_DEC16_ONE_DMA  // 1: stage the tables by LDS-DMA (A/B experiments; slower, see stage_tables)
+#define LAMD_DEC16_ONE_DMA 1
+#endif
+#ifndef LAMD_DEC16_ONE_WAVES  // waves per SIMD the one-pass decoder's register budget is cut for
+#define LAMD_DEC16_ONE_WAVES 4
+#endif
+template <int R, int LW>
+constexpr size_t one_xch_dwords() {
+    constexpr size_t x = Tile<FF16, 8, R, 1, LW, 0, lg_bits(LW)>::kXchDwords;
+    return x > tab16_slot(256) ? x : tab16_slot(256);
+}
+template <int R, int LW, int NZ>
+__global__ void __launch_bounds__((threads_n<8, R, LW>()), LAMD_DEC16_ONE_WAVES) k_dec16n_one(DecArgs a) {
+    if constexpr ((LAMD_ABLATE & 16) != 0) return;
+    constexpr int T = 8, G = lg_bits(LW);
+    using TL = Tile<FF16, T, R, 1, LW, 0, G>;
+    constexpr unsigned NT = threads_n<T, R, LW>(), NW = NT / 64;
+    constexpr size_t kSet = tab16_set_dwords(T);
+    // the exchange area also holds a tile's scale / reveal tables between its
+    // transforms: at narrow strips (LW = 8) it is sized for those
+    constexpr size_t kXch = one_xch_dwords<R, LW>();
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    uint32_t* xch = lds;         // transposes; the scale / reveal tables between them
+    uint32_t* set = lds + kXch;  // skew tables of the current tile
+    uint32_t* slog = set + kSet;           // scale log values of the received tiles (256 a tile)
+    uint32_t* rlog = slog + 8 * 256;       // reveal log values of the output tiles
+    const unsigned wave = uniform(threadIdx.x >> 6), lane64 = threadIdx.x & 63u, lane = threadIdx.x & (LW - 1);
+    const unsigned w0 = (wave << G) | (lane64 >> (6 - G));
+    // 64-byte strips: the two halves of a 128-byte line on one XCD (workgroups
+    // are dealt round-robin over the 8 XCDs: b and b + 8 share one)
+    const unsigned nb = gridDim.x, b = blockIdx.x;
+    const uint64_t strip = (LW < 16 && (nb & 7u) == 0) ? (b & 7u) * (nb >> 3) + (b >> 3) : b;
+    const NarrowCols<LW> cl = narrow_cols<LW>(a.nunits, lane, strip);
+#ifdef LAMD_STAMPS  // 32 stamps per wave: 0 start, 1 first tile staged, per input tile i 2+3i (scale + IFFT), 3+3i (fold), 4+3i (next tile's wait), 26+k output tile k done
+#define STAMP1(k)                                                                                              \
+    do {                                                                                                      \
+        const uint64_t t_ = __builtin_amdgcn_s_memrealtime();                                                 \
+        if ((threadIdx.x & 63) == 0) g_stamps16[(2ull << 22) + (uint64_t(blockIdx.x) * NW + wave) * 32 + (k)] = t_; \
+    } while (0)
+#else
+#define STAMP1(k) \
+    do {          \
+    } while (0)
+#endif
+    [[maybe_unused]] unsigned ti = 0;
+    STAMP1(0);
+    // output slots: tile tile0 + k holds a lost original
+    unsigned live = 0;
+#pragma unroll
+    for (int k = 0; k < NZ; ++k)
+        if (unsigned(k) < a.nout && pyr_bit(a.needed_pyr, T, a.tile0 + k)) live |= 1u << k;
+    // received tiles
+    unsigned have = 0;
+    for (unsigned y = 0; y < a.nlo; ++y)
+        if (pyr_bit(a.present_pyr, T, y)) have |= 1u << y;
+    // prologue: the log values of the scale and reveal multiplies into LDS
+    for (unsigned i = threadIdx.x; i < a.nlo * 256u; i += NT) slog[i] = a.scale_logs[i];
+    for (unsigned i = threadIdx.x; i < unsigned(NZ) * 256u; i += NT)
+        if ((live >> (i >> 8)) & 1u) rlog[i] = a.reveal_logs[((a.tile0 + (i >> 8)) << 8) + (i & 255u)];
+    __syncthreads();
+
+    typename TL::Reg z[NZ], x;
+    // received pieces of tile y: positions [0, R) recovery, [m, m + K)
+    // originals (LeopardFF16.cpp:1715-1730); absent ones read the zero page
+    auto load_tile = [&](unsigned y, unsigned w) {
+        const uint32_t ew = a.erased_dev[(y << 3) + (w >> (5 - R))];
+#pragma unroll
+        for (int r = 0; r < TL::NR; ++r) {
+            const unsigned tp = TL::piece(0, r, w), p = (y << T) + tp;
+            const bool is_rec = p < a.R, is_orig = p >= a.m && p < a.m + a.K;
+            const bool got = !((ew >> (tp & 31)) & 1u) && (is_rec || is_orig);
+            const PieceMap& pm = is_rec ? a.rec : a.orig;
+            const unsigned idx = is_rec ? p : (is_orig ? p - a.m : 0u);
+            const uint8_t* src = got ? (pm.table ? reinterpret_cast<const uint8_t*>(pm.table[idx])
+                                                 : pm.base + uint64_t(idx) * pm.stride) + pm.off
+                                     : a.zeros;
+            ld_unit(x[r], src, got ? cl.off : (cl.off & 31));
+        }
+    };
+#ifdef LAMD_DEC16_ONE_STAGGER
+    // experiment: the second round of workgroups (most likely the second one on
+    // each CU) starts LAMD_DEC16_ONE_STAGGER x 0.1 us late, so the two
+    // workgroups of a CU do not reach their load waits together
+    if (blockIdx.x >= gridDim.x / 2) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__builtin_amdgcn_s_memrealtime() - t0 < uint64_t(LAMD_DEC16_ONE_STAGGER) * 10u) __builtin_amdgcn_s_sleep(8);
+    }
+#endif
+    // the tables of the next phase into LDS: the skew set of tile `sk` (if
+    // sk != ~0u) into set, the multiply tables of log values logs[0, 256) (if
+    // logs) into xch.  Staged through registers (global loads, then LDS
+    // stores) at the tile boundaries, where the tile registers are free: the
+    // 42 KB of one tile's tables land in ~0.5 us this way, against ~4 us for
+    // LDS-DMA (which lands ~25 GB/s per CU, MI355X_MICROARCH.md ldsdma-fill).
+    auto stage_tables = [&](unsigned sk, const uint32_t* logs) {
+#if LAMD_DEC16_ONE_DMA
+#ifndef LAMD_X_NOSKEWDMA
+        if (sk != ~0u) dma_skew_set<NW>(set, a.sktab, sk << T, wave, lane64);
+#endif
+#ifndef LAMD_X_NOLOGDMA
+        if (logs) dma_log_set<NW>(xch, a.tabs, logs, wave, lane64);
+#endif
+        wait_dma();
+#else
+        Tabs16Stage<NT, T> st;
+        LogTabs16Stage<NT, (1u << T)> ls;
+        if (sk != ~0u) st.load(a.sktab, -1, sk << T, 0);
+        if (logs) ls.load(a.tabs, logs);
+        if (sk != ~0u) st.store(set);
+        if (logs) ls.store(xch);
+#endif
+    };
+    // first received tile: pieces, skew set, scale tables
+    unsigned y = have ? unsigned(__builtin_ctz(have)) : a.nlo;
+    if (y < a.nlo) {
+        stage_tables(y, slog + (y << T));
+        __builtin_amdgcn_sched_barrier(0);
+        load_tile(y, w0);
+        __syncthreads();
+    }
+    __builtin_amdgcn_sched_barrier(0);  // the accumulators start here, not across the first staging
+#pragma unroll
+    for (int k = 0; k < NZ; ++k) TL::zero(z[k]);
+    STAMP1(1);
+    while (y < a.nlo) {
+        // an opaque copy of the lane's virtual wave per tile: the per-lane LDS
+        // and table addresses derived from it are recomputed in each tile
+        // instead of being hoisted out of the loop and kept live (k_enc16n)
+        unsigned w = w0;
+        asm volatile("" : "+v"(w));
+        // scale by exp(el[p]) (the zero table for absent positions)
+#pragma unroll
+        for (int r = 0; r < TL::NR; ++r) {
+            asm volatile("" ::: "memory");  // one table live at a time
+            const FF16::Tab t = FF16::tab_lds(xch + tab16_slot(TL::piece(0, r, w)));
+            FF16::mul(x[r], x[r], t);
+#pragma unroll
+            for (int k = 0; k < TL::U; ++k) asm volatile("" : "+v"(x[r][k]));
+        }
+        TL::ifft(x, w, lane, xch, PieceSpace{0, 0, y << T}, LdsWindow16{set, y << T, 0}, AllLive{});
+        STAMP1(2 + 3 * ti);
+        asm volatile("" : "+v"(w));  // the fold's addresses: recomputed, not kept from the IFFT
+        // fold U = x into the output tiles (every branch is workgroup-uniform)
+        static_for<0, NZ>([&](auto K) {
+            constexpr int k = decltype(K)::value;
+            if (!((live >> k) & 1u)) return;
+            const unsigned t = a.tile0 + k;
+            if (t == y) {  // the formal derivative's low bits: D_lo U_t (rs_device.h derivative_add)
+                unsigned wd = w;
+                asm volatile("" : "+v"(wd));
+                TL::derivative_add(z[k], [&](int r, uint32_t* out) { out[0] = x[r][0]; out[1] = x[r][1]; }, wd, lane,
+                                   xch);
+                return;
+            }
+            const uint32_t q = cload(a.qlog + (t ^ y));
+            if (q == kQZero) return;
+            if (q == kQOne) {
+                TL::xor_into(z[k], x);
+                return;
+            }
+            // the multiplier's table through the scalar cache (wave-uniform): SGPRs, of
+            // which v_perm takes one per instruction, so only one dword of each
+            // table pair occupies a VGPR (the LDS copy would hold all 20 in VGPRs
+            // next to the 64 accumulator and 16 tile registers)
+            const FF16::Tab tq = FF16::tab(a.tabs, q);
+#pragma unroll
+            for (int r = 0; r < TL::NR; ++r) {
+                FF16::muladd(z[k][r], x[r], tq);
+                asm volatile("" : "+v"(z[k][r][0]), "+v"(z[k][r][1]));
+                __builtin_amdgcn_sched_barrier(0);  // one multiply-add in flight: the table and 80 accumulators are live
+            }
+        });
+        STAMP1(3 + 3 * ti);
+        // next received tile (or the first output tile's skew set): its pieces,
+        // tables by DMA, one wait
+        const unsigned rest = have & ~((2u << y) - 1u);
+        y = rest ? unsigned(__builtin_ctz(rest)) : a.nlo;
+        __syncthreads();  // every wave is done with set and xch
+        if (y < a.nlo) {
+            // tables first (L2-resident: a short wait), then the pieces, whose
+            // loads are in flight across the barrier: the staging registers
+            // and the tile registers are never live together
+            stage_tables(y, slog + (y << T));
+            __builtin_amdgcn_sched_barrier(0);
+            load_tile(y, w);
+        } else if (live) {
+            stage_tables(a.tile0 + unsigned(__builtin_ctz(live)), nullptr);
+        }
+        __syncthreads();
+        STAMP1(4 + 3 * ti);
+        ++ti;
+    }
+    // output tiles: low FFT, reveal, store the lost originals
+    static_for<0, NZ>([&](auto K) {
+        constexpr int k = decltype(K)::value;
+        if (!((live >> k) & 1u)) return;
+        const unsigned tk = a.tile0 + k;
+        unsigned w = w0;  // opaque per output tile, as in the tile loop
+        asm volatile("" : "+v"(w));
+        TL::fft(z[k], w, lane, xch, PieceSpace{0, 0, tk << T}, LdsWindow16{set, tk << T, 0}, AllLive{});
+        __syncthreads();  // every wave is past the FFT's last exchange and its last table read
+        const unsigned rest = live & ~((2u << k) - 1u);
+        stage_tables(rest ? a.tile0 + unsigned(__builtin_ctz(rest)) : ~0u, rlog + (k << 8));
+        // lost original at p = m + i: work[i] = z[p] * exp(-el[p])  (LeopardFF16.cpp:1771-1773)
+        auto pos = [&](int r) { return (tk << T) + TL::piece(0, r, w); };
+        const uint32_t ew = a.erased_dev[(tk << 3) + (w >> (5 - R))];  // layout 0: one word a lane
+        uint64_t po[TL::NR];
+        lane_ptrs(po, a.out, [&](int r) { return pos(r) >= a.m ? min(pos(r) - a.m, a.K - 1) : 0u; });
+        __syncthreads();
+        if (cl.live) {
+#pragma unroll
+            for (int r = 0; r < TL::NR; ++r) {
+                const unsigned p = pos(r), tp = TL::piece(0, r, w);
+                if (p >= a.m && p < a.m + a.K && ((ew >> (tp & 31)) & 1u)) {
+                    asm volatile("" ::: "memory");
+                    uint32_t o[2];
+                    FF16::mul(o, z[k][r], FF16::tab_lds(xch + tab16_slot(tp)));
+                    st_unit(reinterpret_cast<uint8_t*>(po[r]), cl.off, o);
+                }
+            }
+        }
+        STAMP1(26 + k);
+    });
+}
+#undef STAMP1
+
 template <class Kern>
 hipError_t launch16n(Kern* fn, dim3 grid, unsigned threads, size_t lds_bytes, const DecArgs& a, hipStream_t s) {
     const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
@@ -463,6 +763,20 @@ constexpr size_t kDecFinLds = (DecTL::kXchDwords + kDecNZ * tab16_set_dwords(8))
 static_assert(kDecLds <= 160 * 1024 / 3, "three workgroups per CU");
 static_assert(kDecFinLds <= 160 * 1024 / 2, "two workgroups per CU");
 static_assert(tab16_slot(256) <= DecTL::kXchDwords, "log tables fit the exchange area");
+constexpr int kDecOneNZ = 4;  // output tiles held per lane by the one-pass decoder
+#ifndef LAMD_DEC16_ONE_R
+#define LAMD_DEC16_ONE_R 3
+#endif
+constexpr int kDecOneR = LAMD_DEC16_ONE_R;
+#ifndef LAMD_DEC16_ONE_LW
+#define LAMD_DEC16_ONE_LW 16
+#endif
+// 64-byte strips (one ALTMAP block of every piece), 4-wave workgroups of
+// 8 positions a lane (Z: 64 VGPRs): three workgroups per CU (168 VGPRs, 48 KB
+// of LDS each)
+constexpr int kDecOneLW = LAMD_DEC16_ONE_LW;
+constexpr size_t kDecOneLds = (one_xch_dwords<kDecOneR, kDecOneLW>() + tab16_set_dwords(8) + 8 * 256 + kDecOneNZ * 256) * 4;
+static_assert(kDecOneLW != 8 || kDecOneLds <= 160 * 1024 / 3, "three workgroups per CU");
 }  // namespace
 
 #ifdef LAMD_STAMPS
@@ -486,6 +800,16 @@ bool decode16_small_supported(unsigned Tn) { return Tn >= 9 && Tn <= 11; }
 hipError_t launch_decode16_small_lo(const DecArgs& a, hipStream_t s) {
     const unsigned strips = unsigned((a.nunits + kDecLW - 1) / kDecLW);
     return launch16n(&k_dec16n_lo<kDecR, kDecLW>, dim3(strips, a.nlo), threads_n<8, kDecR, kDecLW>(), kDecLds, a, s);
+}
+// one-pass form: at most kDecOneNZ output tiles
+#ifndef LAMD_DEC16_ONE  // 0: the two-pass form only (A/B experiments)
+#define LAMD_DEC16_ONE 0
+#endif
+bool decode16_one_supported(unsigned nout) { return LAMD_DEC16_ONE && nout <= unsigned(kDecOneNZ); }
+hipError_t launch_decode16_one(const DecArgs& a, hipStream_t s) {
+    const unsigned strips = unsigned((a.nunits + kDecOneLW - 1) / kDecOneLW);
+    return launch16n(&k_dec16n_one<kDecOneR, kDecOneLW, kDecOneNZ>, dim3(strips), threads_n<8, kDecOneR, kDecOneLW>(),
+                     kDecOneLds, a, s);
 }
 hipError_t launch_decode16_small_fin(const DecArgs& a, hipStream_t s) {
     const unsigned strips = unsigned((a.nunits + kDecLW - 1) / kDecLW);

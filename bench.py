@@ -263,6 +263,7 @@ def main():
         breadth = [dict(run_shape(leo, torch, device, k, r, b, loss, n=5),
                         reference_MBps={"encode": re, "decode": rd, "source": "Benchmarks.md:8-27"})
                    for k, r, b, loss, re, rd in BREADTH]
+        secondary.append(dict(ff16_batch(leo, torch, device), kind="ff16_batch"))
     if rank == 0 and not args.no_host:
         host = host_e2e(leo, args.K, args.R, args.bytes)
     if rank == 0 and not args.no_cpu_baseline:
@@ -357,6 +358,10 @@ def config_fracs(secondary, sharded, world):
         if len(secondary) > 3:
             c1p = secondary[3]  # 128+128 x 64 KiB, 16 random losses (partial-loss decoder)
             out["configs1_16loss_decode_us"] = c1p["decode_us"]
+        for sec in secondary:
+            if sec.get("kind") == "ff16_batch":
+                out["ff16_batch_speedup_encode"] = sec["speedup_encode"]
+                out["ff16_batch_speedup_decode"] = sec["speedup_decode"]
     if sharded and world == 1:
         pc = sharded["per_call"]
         out.update({"configs3_encode_ms": pc["encode"]["ms"], "configs3_decode_ms": pc["decode"]["ms"],
@@ -718,6 +723,71 @@ def run_shape(leo, torch, device, k, r, nbytes, loss, n=3):
            "roofline": {"encode": roof("encode", te * 1e6, (k + r) * nbytes),
                         "decode": roof("decode", td * 1e6, (k + loss) * nbytes)}}
     del sets
+    torch.cuda.empty_cache()
+    return res
+
+
+def ff16_batch(leo, torch, device, k=1000, r=200, nbytes=2560, objects=16, loss=200, n=10):
+    """GF(2^16) objects of the breadth shape 1000+200 x 2560 B (Benchmarks.md:
+    17-27): `objects` single leo_encode / leo_decode calls against one
+    leo_amd_encode_batch + one leo_amd_decode_batch over the same objects (one
+    grid per kernel), GPU time per object (HIP events behind a spin kernel)."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_lib as ol
+    lib = leo.lib
+    ewc, dwc = leo.leo_encode_work_count(k, r), leo.leo_decode_work_count(k, r)
+    lo, lr = ol.benchmark_losses(k, r, loss, seed=2, trial=0)
+    data = [hash_fill_cuda(torch, 11 + o, k, nbytes, device) for o in range(objects)]
+    ew = [torch.zeros((ewc, nbytes), dtype=torch.uint8, device=device) for _ in range(objects)]
+    dw = [torch.zeros((dwc, nbytes), dtype=torch.uint8, device=device) for _ in range(objects)]
+    po = [ptrs(d) for d in data]
+    pe = [ptrs(e) for e in ew]
+    pn = [ptrs(d, lost=lo) for d in data]
+    pr = [ptrs(e, r, lost=lr) for e in ew]
+    pd = [ptrs(d) for d in dw]
+    PP = ctypes.POINTER(VP)
+    mk = lambda arrs: (PP * len(arrs))(*[ctypes.cast(a, PP) for a in arrs])  # noqa: E731
+    bo, be, bn, br, bd = mk(po), mk(pe), mk(pn), mk(pr), mk(pd)
+    s = torch.cuda.current_stream(device)
+    leo.set_stream(s.cuda_stream)
+
+    def single_enc():
+        for o in range(objects):
+            assert lib.leo_encode(nbytes, k, r, ewc, po[o], pe[o]) == 0, leo.last_error()
+
+    def single_dec():
+        for o in range(objects):
+            assert lib.leo_decode(nbytes, k, r, dwc, pn[o], pr[o], pd[o]) == 0, leo.last_error()
+
+    def batch_enc():
+        assert lib.leo_amd_encode_batch(objects, nbytes, k, r, ewc, bo, be) == 0, leo.last_error()
+
+    def batch_dec():
+        assert lib.leo_amd_decode_batch(objects, nbytes, k, r, dwc, bn, br, bd) == 0, leo.last_error()
+
+    def t(fn):
+        fn()
+        s.synchronize()
+        a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda._sleep(20_000_000)
+        a.record(s)
+        for _ in range(n):
+            fn()
+        z.record(s)
+        z.synchronize()
+        return a.elapsed_time(z) / 1e3 / n / objects * 1e6  # us per object
+    res = {"workload": f"{objects} objects of {k}+{r} x {nbytes} B (GF(2^16), {loss} originals lost each)",
+           "single_encode_us_per_object": round(t(single_enc), 2), "single_decode_us_per_object": round(t(single_dec), 2),
+           "batch_encode_us_per_object": round(t(batch_enc), 2), "batch_decode_us_per_object": round(t(batch_dec), 2)}
+    for d in dw:
+        d.zero_()
+    batch_dec()
+    idx = torch.tensor(lo, device=device)
+    res["roundtrip_ok"] = all(bool(torch.equal(dw[o].index_select(0, idx), data[o].index_select(0, idx)))
+                              for o in range(objects))
+    res["speedup_encode"] = round(res["single_encode_us_per_object"] / res["batch_encode_us_per_object"], 2)
+    res["speedup_decode"] = round(res["single_decode_us_per_object"] / res["batch_decode_us_per_object"], 2)
+    del data, ew, dw
     torch.cuda.empty_cache()
     return res
 

@@ -228,14 +228,24 @@ struct Workspace {
     hipStream_t pipe_stream[2] = {nullptr, nullptr};
     hipEvent_t in_done[2] = {nullptr, nullptr};
     hipEvent_t out_done[2] = {nullptr, nullptr};
-    // GF(2^16) decoder state kept on the device across calls (its own
-    // allocation, so the arena above can be reused by every other call):
-    // erasure bitmap, the two occupancy pyramids, the error locator and its
-    // FWHT scratch.  dec16_key holds the (K, R, bitmap) the state was built
-    // for: a repeated erasure pattern re-uploads nothing and skips the
-    // error-locator launches.
-    uint8_t* dec16 = nullptr;
-    std::vector<uint32_t> dec16_key;
+    // GF(2^16) decoder states kept on the device across calls (allocations of
+    // their own, so the arena above can be reused by every other call), one
+    // per erasure pattern in kDec16Slots slots: erasure bitmap, the two
+    // occupancy pyramids, the error locator and its FWHT scratch, the scale /
+    // reveal log values.  A slot's key is the (K, R, bitmap) it was built for:
+    // a repeated pattern re-uploads nothing and skips the error-locator
+    // launches.  A new pattern takes the next slot the current call does not
+    // use (a batch holds one per object); slots are rewritten only by later
+    // work on this workspace's stream.
+    struct Dec16Slot {
+        uint8_t* mem = nullptr;
+        std::vector<uint32_t> key;
+        uint64_t stamp = 0;
+    };
+    static constexpr unsigned kDec16Slots = 16;
+    Dec16Slot dec16[kDec16Slots];
+    uint64_t dec16_call = 0;
+    unsigned dec16_next = 0;
     // Device rows of a host call staged by direct SDMA copies (run_host_direct).
     uint8_t* direct = nullptr;
     size_t direct_size = 0;
@@ -278,7 +288,11 @@ struct Workspace {
             if (sl.done) (void)hipEventDestroy(sl.done);
             sl = StageSlot{};
         }
-        release_device_memory(dev, {dbuf, dec16, ring_dev, direct, el8});
+        release_device_memory(dev, {dbuf, ring_dev, direct, el8});
+        for (Dec16Slot& d : dec16) {
+            release_device_memory(dev, {d.mem});
+            d = Dec16Slot{};
+        }
         el8 = nullptr;
         el8_map.clear();
         el8_key.clear();
@@ -293,7 +307,7 @@ struct Workspace {
             in_done[s] = out_done[s] = nullptr;
         }
         if (last_use) (void)hipEventDestroy(last_use);
-        dbuf = dec16 = ring_dev = ring_host = ring_host_dev = direct = nullptr;
+        dbuf = ring_dev = ring_host = ring_host_dev = direct = nullptr;
         last_use = nullptr;
         dsize = slot_bytes = direct_size = 0;
     }
@@ -343,6 +357,33 @@ struct Workspace {
         dsize = 0;
         HIP_OK(pool_alloc(reinterpret_cast<void**>(&dbuf), want, dev, stream), "allocate scratch");
         dsize = want;
+        return Leopard_Success;
+    }
+    // The decoder-state slot of pattern `key` for the current call (++dec16_call
+    // first): *fresh when it must be built.  Fails when every slot is taken by
+    // the current call (callers keep to kDec16Slots patterns a call).
+    LeopardResult dec16_slot(std::vector<uint32_t>& key, size_t bytes, unsigned* idx, bool* fresh) {
+        touched = true;
+        for (unsigned i = 0; i < kDec16Slots; ++i)
+            if (dec16[i].mem && dec16[i].key == key) {
+                dec16[i].stamp = dec16_call;
+                *idx = i;
+                *fresh = false;
+                return Leopard_Success;
+            }
+        unsigned tries = 0;
+        while (dec16[dec16_next].stamp == dec16_call && tries++ < kDec16Slots) dec16_next = (dec16_next + 1) % kDec16Slots;
+        if (tries > kDec16Slots) {
+            tls.last_error = "too many erasure patterns in one call";
+            return Leopard_InvalidInput;
+        }
+        Dec16Slot& d = dec16[dec16_next];
+        if (!d.mem) HIP_OK(pool_alloc(reinterpret_cast<void**>(&d.mem), bytes, dev, stream), "allocate decoder state");
+        d.key.swap(key);
+        d.stamp = dec16_call;
+        *idx = dec16_next;
+        *fresh = true;
+        dec16_next = (dec16_next + 1) % kDec16Slots;
         return Leopard_Success;
     }
     // Starts a call's use of the error-locator cache (slots it takes stay put until the next call).
@@ -915,6 +956,87 @@ LeopardResult decode_device8(Call& c, uint64_t bytes, uint64_t off, unsigned K, 
     return Leopard_Success;
 }
 
+// GF(2^16) decoder state of one erasure pattern (a workspace slot): erasure
+// bitmap over 65536 positions, occupancy pyramids for pruning (received data /
+// lost originals), the error locator and the per-position log values of the
+// scale and reveal multiplies -- uploaded and computed on the device only when
+// the slot is new for this pattern.  Fills a's shape and state fields.
+constexpr size_t kDec16Bitmap = 65536 / 32;
+constexpr size_t kDec16OffPyr = kDec16Bitmap * 4;
+constexpr size_t kDec16OffTmp = kDec16OffPyr + (2 * kPyrWords * 4 + 255) / 256 * 256;
+constexpr size_t kDec16OffEl = kDec16OffTmp + 65536 * 4;
+constexpr size_t kDec16OffSl = kDec16OffEl + 65536 * 4;
+constexpr size_t kDec16OffRl = kDec16OffSl + 65536 * 4;
+constexpr size_t kDec16Bytes = kDec16OffRl + 65536 * 4;
+LeopardResult dec16_state(Call& c, unsigned K, unsigned R, const void* const* orig, const void* const* rec,
+                          DecArgs& a) {
+    const unsigned m = next_pow2(R);
+    const unsigned n = next_pow2(m + K);
+    // error_locations[] = 1 at lost recoveries, [R, m), lost originals (LeopardFF8.cpp:1825-1840)
+    std::vector<uint32_t> key(2 + kDec16Bitmap, 0);
+    key[0] = K;
+    key[1] = R;
+    uint32_t* erased = key.data() + 2;
+    auto set = [&](unsigned p) { erased[p >> 5] |= 1u << (p & 31); };
+    for (unsigned i = 0; i < R; ++i)
+        if (!rec[i]) set(i);
+    for (unsigned i = R; i < m; ++i) set(i);
+    for (unsigned i = 0; i < K; ++i)
+        if (!orig[i]) set(m + i);
+    const unsigned words = (std::max(n, 256u) + 31) / 32;
+    std::vector<uint32_t> bitmap(erased, erased + words);
+    Workspace& ws = *c.ws;
+    unsigned si = 0;
+    bool fresh = false;
+    LeopardResult r = ws.dec16_slot(key, kDec16Bytes, &si, &fresh);
+    if (r != Leopard_Success) return r;
+    uint8_t* st = ws.dec16[si].mem;
+    if (fresh) {
+        ws.dec16[si].key.clear();  // stays invalid unless the uploads and launches below succeed
+        r = ws.upload(st, kDec16OffTmp, c.s, [&](uint8_t* h) {
+            std::memset(h, 0, kDec16OffTmp);
+            std::memcpy(h, bitmap.data(), bitmap.size() * 4);
+            uint32_t* pp = reinterpret_cast<uint32_t*>(h + kDec16OffPyr);
+            uint32_t* pn = pp + kPyrWords;
+            auto mark = [](uint32_t* pyr, unsigned p) {
+                for (unsigned L = 0; L <= 16; ++L) {
+                    const unsigned j = p >> L;
+                    pyr[pyr_offset(L) + (j >> 5)] |= 1u << (j & 31);
+                }
+            };
+            for (unsigned i = 0; i < R; ++i)
+                if (rec[i]) mark(pp, i);
+            for (unsigned i = 0; i < K; ++i) mark(orig[i] ? pp : pn, m + i);
+        });
+        if (r != Leopard_Success) return r;
+        HIP_OK(launch_error_locator16(reinterpret_cast<uint32_t*>(st), c.t->walsh16,
+                                      reinterpret_cast<uint32_t*>(st + kDec16OffTmp),
+                                      reinterpret_cast<uint32_t*>(st + kDec16OffEl),
+                                      reinterpret_cast<uint32_t*>(st + kDec16OffSl),
+                                      reinterpret_cast<uint32_t*>(st + kDec16OffRl), m, K, R, c.s),
+               "error locator");
+        ws.dec16[si].key.assign(2 + kDec16Bitmap, 0);
+        ws.dec16[si].key[0] = K;
+        ws.dec16[si].key[1] = R;
+        std::copy(bitmap.begin(), bitmap.end(), ws.dec16[si].key.begin() + 2);
+    }
+    a.sktab = c.t->sktab16;
+    a.tabs = c.t->tab16;
+    a.zeros = c.t->zeros;
+    a.walsh = c.t->walsh16;
+    a.K = K;
+    a.R = R;
+    a.m = m;
+    a.Tn = log2u(n);
+    a.el = reinterpret_cast<uint32_t*>(st + kDec16OffEl);
+    a.scale_logs = reinterpret_cast<uint32_t*>(st + kDec16OffSl);
+    a.reveal_logs = reinterpret_cast<uint32_t*>(st + kDec16OffRl);
+    a.erased_dev = reinterpret_cast<uint32_t*>(st);
+    a.present_pyr = reinterpret_cast<uint32_t*>(st + kDec16OffPyr);
+    a.needed_pyr = a.present_pyr + kPyrWords;
+    return Leopard_Success;
+}
+
 LeopardResult decode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, unsigned R, const void* const* orig,
                             const void* const* rec, void** work) {
     const unsigned m = next_pow2(R);
@@ -923,51 +1045,13 @@ LeopardResult decode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
     const unsigned Tn = log2u(n);
     if (!ff16) return decode_device8(c, bytes, off, K, R, orig, rec, work);
 
-    // error_locations[] = 1 at lost recoveries, [R, m), lost originals (LeopardFF8.cpp:1825-1840)
-    std::vector<uint32_t> erased((std::max(n, 256u) + 31) / 32, 0);
-    auto set = [&](unsigned p) { erased[p >> 5] |= 1u << (p & 31); };
-    for (unsigned i = 0; i < R; ++i)
-        if (!rec[i]) set(i);
-    for (unsigned i = R; i < m; ++i) set(i);
-    for (unsigned i = 0; i < K; ++i)
-        if (!orig[i]) set(m + i);
-
     DecArgs a;
     std::memset(&a, 0, sizeof(a));
     MapBuilder mb;
     mb.build(a.orig, orig, K, off);
     mb.build(a.rec, rec, R, off);
     mb.build(a.out, work, K, off);
-    a.sktab = c.t->sktab16;
-    a.tabs = c.t->tab16;
-    a.zeros = c.t->zeros;
-    a.walsh = c.t->walsh16;
-    a.K = K;
-    a.R = R;
-    a.m = m;
-    a.Tn = Tn;
-
-    // FF16: erasure bitmap (full 65536 positions) + error locator on the device,
-    // plus occupancy pyramids for pruning (received data / lost originals), in
-    // the workspace's persistent decoder state (rebuilt only when the erasure
-    // pattern changes).
-    const size_t bitmap_words = 65536 / 32;
-    const size_t off_pyr = bitmap_words * 4;
-    const size_t pyr_bytes = (2 * kPyrWords * 4 + 255) / 256 * 256;
-    const size_t off_tmp = off_pyr + pyr_bytes;
-    const size_t off_el = off_tmp + 65536 * 4;
-    const size_t off_sl = off_el + 65536 * 4;
-    const size_t off_rl = off_sl + 65536 * 4;
-    const size_t dec16_bytes = off_rl + 65536 * 4;
     Workspace& ws = *c.ws;
-    ws.touched = true;
-    if (!ws.dec16)
-        HIP_OK(pool_alloc(reinterpret_cast<void**>(&ws.dec16), dec16_bytes, ws.dev, c.s), "allocate decoder state");
-    std::vector<uint32_t> key(2 + bitmap_words, 0);
-    key[0] = K;
-    key[1] = R;
-    std::copy(erased.begin(), erased.end(), key.begin() + 2);
-    const bool rebuild = key != ws.dec16_key;
 
     // Narrow columns and n <= 2048: the two-pass narrow-strip decoder
     // (rs_ff16_small.hip), whose only intermediate is U (tiles with received data).
@@ -984,45 +1068,10 @@ LeopardResult decode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
     const size_t off_slab = table_bytes;
     LeopardResult r = ws.reserve_device(off_slab + slab_pieces * slice);
     if (r != Leopard_Success) return r;
-    // piece tables (if any), and on a new pattern the bitmap + pyramids
-    r = mb.flush(ws, reinterpret_cast<uint64_t*>(ws.dbuf), c.s);
+    r = mb.flush(ws, reinterpret_cast<uint64_t*>(ws.dbuf), c.s);  // piece tables (if any)
     if (r != Leopard_Success) return r;
-    if (rebuild) {
-        r = ws.upload(ws.dec16, off_tmp, c.s, [&](uint8_t* h) {
-            std::memset(h, 0, off_tmp);
-            std::memcpy(h, erased.data(), erased.size() * 4);
-            uint32_t* pp = reinterpret_cast<uint32_t*>(h + off_pyr);
-            uint32_t* pn = pp + kPyrWords;
-            auto mark = [](uint32_t* pyr, unsigned p) {
-                for (unsigned L = 0; L <= 16; ++L) {
-                    const unsigned j = p >> L;
-                    pyr[pyr_offset(L) + (j >> 5)] |= 1u << (j & 31);
-                }
-            };
-            for (unsigned i = 0; i < R; ++i)
-                if (rec[i]) mark(pp, i);
-            for (unsigned i = 0; i < K; ++i) mark(orig[i] ? pp : pn, m + i);
-        });
-        if (r != Leopard_Success) return r;
-    }
-
-    uint32_t* d_bitmap = reinterpret_cast<uint32_t*>(ws.dec16);
-    uint32_t* d_tmp = reinterpret_cast<uint32_t*>(ws.dec16 + off_tmp);
-    uint32_t* d_el = reinterpret_cast<uint32_t*>(ws.dec16 + off_el);
-    uint32_t* d_sl = reinterpret_cast<uint32_t*>(ws.dec16 + off_sl);
-    uint32_t* d_rl = reinterpret_cast<uint32_t*>(ws.dec16 + off_rl);
-    if (rebuild) {
-        ws.dec16_key.clear();  // stays invalid if the launch fails
-        HIP_OK(launch_error_locator16(d_bitmap, c.t->walsh16, d_tmp, d_el, d_sl, d_rl, m, K, R, c.s),
-               "error locator");
-        ws.dec16_key = std::move(key);
-    }
-    a.el = d_el;
-    a.scale_logs = d_sl;
-    a.reveal_logs = d_rl;
-    a.erased_dev = d_bitmap;
-    a.present_pyr = reinterpret_cast<uint32_t*>(ws.dec16 + off_pyr);
-    a.needed_pyr = a.present_pyr + kPyrWords;
+    ++ws.dec16_call;
+    if ((r = dec16_state(c, K, R, orig, rec, a)) != Leopard_Success) return r;
     a.nlo = (m + K + (1u << kLoBits) - 1) >> kLoBits;
     // No original survives and n = 2m: the received pieces fill only the low half
     // (k_dec_hi_half); pass 1 then runs the recovery tiles only.
@@ -1895,6 +1944,97 @@ LeopardResult run_batch8(int dev, unsigned count, Fill fill, Launch launch) {
 // objects (erasure patterns: one error-locator slot each) per batched GF(2^8) decode launch
 constexpr unsigned kDecBatchChunk = Workspace::kEl8Slots / 2;
 
+// GF(2^16) batches on narrow strips (pieces <= 256 KiB): the encoder for
+// m = 128, 256 (k_enc16n) and the two-pass decoder for n <= 2048 run one grid
+// per kernel over every object (blockIdx.y / .z = object, argument blocks
+// uploaded through the staging ring), so a batch of small objects fills the
+// GPU where one call of 2560-byte pieces is 20 column strips.
+bool narrow_encode16(unsigned K, unsigned R, uint64_t bytes) {
+    const unsigned m = next_pow2(R), n = next_pow2(m + K);
+    return K > 1 && R > 1 && n > 256 && encode16_small_supported(log2u(m)) && bytes <= kNarrowColumnsMax;
+}
+bool narrow_decode16(unsigned K, unsigned R, uint64_t bytes) {
+    const unsigned m = next_pow2(R), n = next_pow2(m + K);
+    return n > 256 && g_q16_ok && decode16_small_supported(log2u(n)) && bytes <= kNarrowColumnsMax;
+}
+
+LeopardResult encode_batch16(int dev, unsigned count, uint64_t bytes, unsigned K, unsigned R,
+                             const void* const* const* orig, void** const* work) {
+    DeviceGuard guard(dev);
+    Call c;
+    LeopardResult r = begin_call(dev, c);
+    if (r != Leopard_Success) return r;
+    const unsigned m = next_pow2(R), Tm = log2u(m);
+    std::vector<EncArgs> args(count);  // sized up front: mb keeps pointers to the maps
+    MapBuilder mb;
+    for (unsigned o = 0; o < count; ++o) {
+        EncArgs& a = args[o];
+        std::memset(&a, 0, sizeof(a));
+        mb.build(a.in, orig[o], K, 0);
+        mb.build(a.out, work[o], R, 0);
+        a.sktab = c.t->sktab16;
+        a.tabs = c.t->tab16;
+        a.zeros = c.t->zeros;
+        a.fused = c.t->fused16 + fused16_base(Tm);
+        a.K = K;
+        a.R = R;
+        a.Tm = Tm;
+        a.nchunks = (K + m - 1) / m;
+        a.nunits = bytes / 8;
+    }
+    const size_t table_bytes = (mb.bytes() + 255) / 256 * 256;
+    if ((r = c.ws->reserve_device(table_bytes + count * sizeof(EncArgs))) != Leopard_Success) return r;
+    if ((r = mb.flush(*c.ws, reinterpret_cast<uint64_t*>(c.ws->dbuf), c.s)) != Leopard_Success) return r;
+    EncArgs* dargs = reinterpret_cast<EncArgs*>(c.ws->dbuf + table_bytes);
+    if ((r = c.ws->upload(dargs, args.data(), count * sizeof(EncArgs), c.s)) != Leopard_Success) return r;
+    HIP_OK(launch_encode16_small_batch(Tm, dargs, count, bytes / 8, c.s), "batch encode kernel");
+    return finish(c, false);
+}
+
+// Decoder: objects in chunks of kDec16Slots (each object's erasure pattern
+// holds a decoder-state slot for the chunk), a U slab per object.
+LeopardResult decode_batch16(int dev, unsigned count, uint64_t bytes, unsigned K, unsigned R,
+                             const void* const* const* orig, const void* const* const* rec, void** const* work) {
+    DeviceGuard guard(dev);
+    Call c;
+    LeopardResult r = begin_call(dev, c);
+    if (r != Leopard_Success) return r;
+    Workspace& ws = *c.ws;
+    const unsigned m = next_pow2(R), n = next_pow2(m + K), Tn = log2u(n);
+    const unsigned ntiles_in = (m + K + (1u << kLoBits) - 1) >> kLoBits;
+    const unsigned tile0 = m >> kLoBits, nout = ((m + K - 1) >> kLoBits) - tile0 + 1;
+    const uint64_t slab = (uint64_t(ntiles_in) << kLoBits) * bytes;  // U of one object
+    for (unsigned o0 = 0; o0 < count; o0 += Workspace::kDec16Slots) {
+        const unsigned nb = std::min(Workspace::kDec16Slots, count - o0);
+        ++ws.dec16_call;
+        std::vector<DecArgs> args(nb);
+        MapBuilder mb;
+        for (unsigned o = 0; o < nb; ++o) {
+            DecArgs& a = args[o];
+            std::memset(&a, 0, sizeof(a));
+            mb.build(a.orig, orig[o0 + o], K, 0);
+            mb.build(a.rec, rec[o0 + o], R, 0);
+            mb.build(a.out, work[o0 + o], K, 0);
+            if ((r = dec16_state(c, K, R, orig[o0 + o], rec[o0 + o], a)) != Leopard_Success) return r;
+            a.nlo = ntiles_in;
+            a.qlog = c.t->qlog16 + high_q16_base(Tn - kLoBits);
+            a.tile0 = tile0;
+            a.nout = nout;
+            a.nunits = bytes / 8;
+        }
+        const size_t table_bytes = (mb.bytes() + 255) / 256 * 256;
+        const size_t args_bytes = (nb * sizeof(DecArgs) + 255) / 256 * 256;
+        if ((r = ws.reserve_device(table_bytes + args_bytes + nb * slab)) != Leopard_Success) return r;
+        if ((r = mb.flush(ws, reinterpret_cast<uint64_t*>(ws.dbuf), c.s)) != Leopard_Success) return r;
+        for (unsigned o = 0; o < nb; ++o)
+            args[o].a_out = args[o].a_in = PieceMap{nullptr, ws.dbuf + table_bytes + args_bytes + o * slab, bytes, 0};
+        DecArgs* dargs = reinterpret_cast<DecArgs*>(ws.dbuf + table_bytes);
+        if ((r = ws.upload(dargs, args.data(), nb * sizeof(DecArgs), c.s)) != Leopard_Success) return r;
+        HIP_OK(launch_decode16_small_batch(dargs, nb, bytes / 8, ntiles_in, nout, c.s), "batch decode kernels");
+    }
+    return finish(c, false);
+}
+
 LeopardResult encode_batch(unsigned count, uint64_t bytes, unsigned K, unsigned R, unsigned work_count,
                            const void* const* const* orig, void** const* work) {
     if (!orig || !work) return Leopard_InvalidInput;
@@ -1928,6 +2068,18 @@ LeopardResult encode_batch(unsigned count, uint64_t bytes, unsigned K, unsigned 
                 [&](const Ff8EncArgs* d, int, hipStream_t s) {
                     return launch_ff8_encode_batch(Tm, d, count, uint32_t(bytes / 4), multi, form, s);
                 });
+    }
+    if (narrow_encode16(K, R, bytes)) {
+        MemKind k16 = MemKind::Host;
+        const int d16 = pick_device(orig[0][0], &k16);
+        if (k16 == MemKind::Device) {
+            RangeCache rc;
+            bool on_dev = true;
+            for (unsigned o = 0; o < count && on_dev; ++o)
+                on_dev = rc.all_on(orig[o], K, bytes, d16) &&
+                         rc.all_on(const_cast<const void* const*>(work[o]), R, bytes, d16);
+            if (on_dev) return encode_batch16(d16, count, bytes, K, R, orig, work);
+        }
     }
     for (unsigned o = 0; o < count; ++o) {
         const LeopardResult r = encode_any(bytes, 0, K, R, orig[o], work[o]);
@@ -2017,6 +2169,23 @@ LeopardResult decode_batch(unsigned count, uint64_t bytes, unsigned K, unsigned 
                 if (r != Leopard_Success) return r;
             }
             return Leopard_Success;
+        }
+    }
+    if (general && narrow_decode16(K, R, bytes)) {
+        const void* first = nullptr;  // the device rule of decode_any
+        for (unsigned i = 0; i < K && !first; ++i) first = orig[0][i];
+        for (unsigned i = 0; i < R && !first; ++i) first = rec[0][i];
+        MemKind k16 = MemKind::Host;
+        const int d16 = pick_device(first, &k16);
+        if (k16 == MemKind::Device) {
+            RangeCache rc;
+            bool on_dev = true;
+            for (unsigned o = 0; o < count && on_dev; ++o) {
+                on_dev = rc.all_on(orig[o], K, bytes, d16) && rc.all_on(rec[o], R, bytes, d16);
+                for (unsigned i = 0; i < K && on_dev; ++i)
+                    if (!orig[o][i]) on_dev = rc.on(work[o][i], bytes, d16);
+            }
+            if (on_dev) return decode_batch16(d16, count, bytes, K, R, orig, rec, work);
         }
     }
     for (unsigned o = 0; o < count; ++o) {

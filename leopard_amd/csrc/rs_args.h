@@ -167,6 +167,12 @@ hipError_t launch_encode16_small(unsigned Tm, const EncArgs& a, hipStream_t s);
 bool decode16_small_supported(unsigned Tn);
 hipError_t launch_decode16_small_lo(const DecArgs& a, hipStream_t s);
 hipError_t launch_decode16_small_fin(const DecArgs& a, hipStream_t s);
+// batches of `count` objects of one shape, argument blocks in device memory
+// (object = blockIdx.y; pass 1 of the decoder: blockIdx.z)
+hipError_t launch_encode16_small_batch(unsigned Tm, const EncArgs* objs, unsigned count, uint64_t nunits,
+                                       hipStream_t s);
+hipError_t launch_decode16_small_batch(const DecArgs* objs, unsigned count, uint64_t nunits, unsigned nlo,
+                                       unsigned nout, hipStream_t s);
 // one pass (scale + low IFFT per received tile folded into per-lane Z
 // accumulators, then low FFT + reveal per output tile) when nout is small
 bool decode16_one_supported(unsigned nout);

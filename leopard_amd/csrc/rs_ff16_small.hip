@@ -100,7 +100,7 @@ constexpr unsigned threads_n() { return 64u << (T - R - lg_bits(LW)); }
 // ------------------------------------------------------------------ encode --
 
 template <int T, int R, int LW>
-__global__ void __launch_bounds__((threads_n<T, R, LW>()), 4) k_enc16n(EncArgs a) {
+LDEV void enc16n_body(const EncArgs& a) {
     if constexpr ((LAMD_ABLATE & 16) != 0) return;
     constexpr int G = lg_bits(LW);
     static_assert(T - R - G >= 0, "at least one wave");
@@ -196,6 +196,17 @@ __global__ void __launch_bounds__((threads_n<T, R, LW>()), 4) k_enc16n(EncArgs a
 }
 
 template <int T, int R, int LW>
+__global__ void __launch_bounds__((threads_n<T, R, LW>()), 4) k_enc16n(EncArgs a) {
+    enc16n_body<T, R, LW>(a);
+}
+// Batched launch (leo_amd_encode_batch): object blockIdx.y of an array of
+// argument blocks in device memory, one grid over every object's strips.
+template <int T, int R, int LW>
+__global__ void __launch_bounds__((threads_n<T, R, LW>()), 4) k_enc16n_batch(const EncArgs* __restrict__ objs) {
+    enc16n_body<T, R, LW>(objs[blockIdx.y]);
+}
+
+template <int T, int R, int LW>
 hipError_t launch_enc16n(const EncArgs& a, hipStream_t s) {
     using TL = Tile<FF16, T, R, 1, LW, 0, lg_bits(LW)>;
     constexpr size_t lds = (TL::kXchDwords + 2 * tab16_set_dwords(T)) * 4;
@@ -233,12 +244,11 @@ LDEV bool pyr_bit(const uint32_t* pyr, unsigned L, unsigned j) {
 constexpr uint32_t kQZero = 0xFFFFFFFFu, kQOne = 0xFFFFFFFEu;  // q entries that are 0 / 1 (else a log value)
 
 template <int R, int LW>
-__global__ void __launch_bounds__((threads_n<8, R, LW>()), 4) k_dec16n_lo(DecArgs a) {
+LDEV void dec16n_lo_body(const DecArgs& a, const unsigned y) {
     if constexpr ((LAMD_ABLATE & 16) != 0) return;
     constexpr int T = 8, G = lg_bits(LW);
     using TL = Tile<FF16, T, R, 1, LW, 0, G>;
     constexpr unsigned NT = threads_n<T, R, LW>();
-    const unsigned y = blockIdx.y;
     if (!pyr_bit(a.present_pyr, T, y)) return;  // nothing received in this tile: U_y = 0, pass 2 skips it
     [[maybe_unused]] constexpr uint64_t kStampBase = 0;
     STAMP16(0);
@@ -297,6 +307,16 @@ __global__ void __launch_bounds__((threads_n<8, R, LW>()), 4) k_dec16n_lo(DecArg
     STAMP16(4);
 }
 
+template <int R, int LW>
+__global__ void __launch_bounds__((threads_n<8, R, LW>()), 4) k_dec16n_lo(DecArgs a) {
+    dec16n_lo_body<R, LW>(a, blockIdx.y);
+}
+// batched: tile blockIdx.y of object blockIdx.z (argument blocks in device memory)
+template <int R, int LW>
+__global__ void __launch_bounds__((threads_n<8, R, LW>()), 4) k_dec16n_lo_batch(const DecArgs* __restrict__ objs) {
+    dec16n_lo_body<R, LW>(objs[blockIdx.z], blockIdx.y);
+}
+
 // Pass 2 over NZ consecutive output tiles per workgroup: every U tile is read
 // once for all of them and its perm selectors are formed once for all of their
 // multiplies.  NZ = 2 measured slower than 1 (its registers allow one
@@ -310,7 +330,7 @@ __global__ void __launch_bounds__((threads_n<8, R, LW>()), 4) k_dec16n_lo(DecArg
 #define LAMD_DEC16N_FIN_WAVES (LAMD_DEC16N_NZ > 1 ? 3 : 4)
 #endif
 template <int R, int LW, int NZ>
-__global__ void __launch_bounds__((threads_n<8, R, LW>()), LAMD_DEC16N_FIN_WAVES) k_dec16n_fin(DecArgs a) {
+LDEV void dec16n_fin_body(const DecArgs& a) {
     if constexpr ((LAMD_ABLATE & 16) != 0) return;
     constexpr int T = 8, G = lg_bits(LW);
     using TL = Tile<FF16, T, R, 1, LW, 0, G>;
@@ -747,6 +767,17 @@ __global__ void __launch_bounds__((threads_n<8, R, LW>()), LAMD_DEC16_ONE_WAVES)
 }
 #undef STAMP1
 
+template <int R, int LW, int NZ>
+__global__ void __launch_bounds__((threads_n<8, R, LW>()), LAMD_DEC16N_FIN_WAVES) k_dec16n_fin(DecArgs a) {
+    dec16n_fin_body<R, LW, NZ>(a);
+}
+// batched: object blockIdx.y
+template <int R, int LW, int NZ>
+__global__ void __launch_bounds__((threads_n<8, R, LW>()), LAMD_DEC16N_FIN_WAVES)
+    k_dec16n_fin_batch(const DecArgs* __restrict__ objs) {
+    dec16n_fin_body<R, LW, NZ>(objs[blockIdx.y]);
+}
+
 template <class Kern>
 hipError_t launch16n(Kern* fn, dim3 grid, unsigned threads, size_t lds_bytes, const DecArgs& a, hipStream_t s) {
     const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
@@ -795,6 +826,27 @@ hipError_t launch_encode16_small(unsigned Tm, const EncArgs& a, hipStream_t s) {
     }
 }
 
+// Batches of `count` objects of one shape: argument blocks in device memory.
+hipError_t launch_encode16_small_batch(unsigned Tm, const EncArgs* objs, unsigned count, uint64_t nunits,
+                                       hipStream_t s) {
+    auto go = [&](auto fn, unsigned threads, size_t lds) {
+        const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
+                                                    hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+        if (attr != hipSuccess) return attr;
+        const EncArgs* arg = objs;
+        void* params[] = {&arg};
+        return hipLaunchKernel(reinterpret_cast<const void*>(fn), dim3(unsigned((nunits + 15) / 16), count),
+                               dim3(threads), params, lds, s);
+    };
+    using TL7 = Tile<FF16, 7, 3, 1, 16, 0, lg_bits(16)>;
+    using TL8 = Tile<FF16, 8, 3, 1, 16, 0, lg_bits(16)>;
+    switch (Tm) {
+        case 7: return go(&k_enc16n_batch<7, 3, 16>, threads_n<7, 3, 16>(), (TL7::kXchDwords + 2 * tab16_set_dwords(7)) * 4);
+        case 8: return go(&k_enc16n_batch<8, 3, 16>, threads_n<8, 3, 16>(), (TL8::kXchDwords + 2 * tab16_set_dwords(8)) * 4);
+        default: return hipErrorInvalidValue;
+    }
+}
+
 // n = 2^Tn, 9 <= Tn <= 11 (2 .. 8 tiles of 256 positions)
 bool decode16_small_supported(unsigned Tn) { return Tn >= 9 && Tn <= 11; }
 hipError_t launch_decode16_small_lo(const DecArgs& a, hipStream_t s) {
@@ -810,6 +862,26 @@ hipError_t launch_decode16_one(const DecArgs& a, hipStream_t s) {
     const unsigned strips = unsigned((a.nunits + kDecOneLW - 1) / kDecOneLW);
     return launch16n(&k_dec16n_one<kDecOneR, kDecOneLW, kDecOneNZ>, dim3(strips), threads_n<8, kDecOneR, kDecOneLW>(),
                      kDecOneLds, a, s);
+}
+// both passes over `count` objects of one shape (same nlo, nout, column count)
+hipError_t launch_decode16_small_batch(const DecArgs* objs, unsigned count, uint64_t nunits, unsigned nlo,
+                                       unsigned nout, hipStream_t s) {
+    const unsigned strips = unsigned((nunits + kDecLW - 1) / kDecLW);
+    const DecArgs* arg = objs;
+    void* params[] = {&arg};
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dec16n_lo_batch<kDecR, kDecLW>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, int(kDecLds));
+    if (e != hipSuccess) return e;
+    e = hipLaunchKernel(reinterpret_cast<const void*>(&k_dec16n_lo_batch<kDecR, kDecLW>), dim3(strips, nlo, count),
+                        dim3(threads_n<8, kDecR, kDecLW>()), params, kDecLds, s);
+    if (e != hipSuccess) return e;
+    const unsigned groups = (strips + 7) / 8;
+    const unsigned ngrp = (nout + kDecNZ - 1) / kDecNZ;
+    e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dec16n_fin_batch<kDecR, kDecLW, kDecNZ>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, int(kDecFinLds));
+    if (e != hipSuccess) return e;
+    return hipLaunchKernel(reinterpret_cast<const void*>(&k_dec16n_fin_batch<kDecR, kDecLW, kDecNZ>),
+                           dim3(groups * 8 * ngrp, count), dim3(threads_n<8, kDecR, kDecLW>()), params, kDecFinLds, s);
 }
 hipError_t launch_decode16_small_fin(const DecArgs& a, hipStream_t s) {
     const unsigned strips = unsigned((a.nunits + kDecLW - 1) / kDecLW);

@@ -542,7 +542,8 @@ def _batch_objects(k, r, b, count, seed):
 @pytest.mark.parametrize("k,r,b,layout", [(128, 128, 4096, "slab"), (128, 128, 4096, "shuffled"),
                                           (100, 20, 64 * 37, "slab"), (100, 20, 64 * 37, "shuffled"),
                                           (200, 55, 1024, "slab"), (1000, 200, 256, "slab"), (16, 16, 256, "slab"),
-                                          (100, 70, 512, "slab")])
+                                          (100, 70, 512, "slab"), (1000, 200, 2560, "shuffled"),
+                                          (300, 100, 640, "slab"), (1000, 1000, 320, "slab")])
 def test_batch_encode_decode_match_oracle(leo, k, r, b, layout):
     """leo_amd_encode_batch / decode_batch (one launch over every object for
     GF(2^8); object by object otherwise) == independent calls == the oracle.
@@ -550,8 +551,10 @@ def test_batch_encode_decode_match_oracle(leo, k, r, b, layout):
     objects: 16+16 runs 70 objects), shuffled piece orders through the
     uploaded argument blocks.  The decode batch mixes erasure patterns: full
     loss (half-position decoder), partial losses, and objects with lost
-    recovery pieces."""
-    count = 70 if k == 16 else 5
+    recovery pieces.  GF(2^16) objects on narrow strips (m <= 256 encode,
+    n <= 2048 decode) also run one grid per kernel; 20 of them span two
+    decoder-state chunks (16 erasure patterns a launch pair)."""
+    count = 70 if k == 16 else 20 if k + r > 256 else 5
     objs = _batch_objects(k, r, b, count, k + r)
     wc, dwc = leo.leo_encode_work_count(k, r), leo.leo_decode_work_count(k, r)
     if layout == "slab":

@@ -246,9 +246,13 @@ struct Workspace {
     Dec16Slot dec16[kDec16Slots];
     uint64_t dec16_call = 0;
     unsigned dec16_next = 0;
-    // Device rows of a host call staged by direct SDMA copies (run_host_direct).
+    // Device rows of a host call staged by direct SDMA copies (run_host_direct),
+    // and the side streams its column slices run on (with their events).
     uint8_t* direct = nullptr;
     size_t direct_size = 0;
+    static constexpr int kSideStreams = 3;
+    hipStream_t side[kSideStreams] = {nullptr, nullptr, nullptr};
+    hipEvent_t side_ev[kSideStreams + 1] = {nullptr, nullptr, nullptr, nullptr};
     // GF(2^8) error locators by erasure pattern (k_el8's outputs): kEl8Slots
     // slots of 256 bytes on the device.  A pattern seen before launches
     // nothing; a new one takes the next slot that the current call does not
@@ -306,6 +310,17 @@ struct Workspace {
             pipe_stream[s] = nullptr;
             in_done[s] = out_done[s] = nullptr;
         }
+        for (int i = 0; i < kSideStreams; ++i)
+            if (side[i]) {
+                (void)hipStreamSynchronize(side[i]);
+                (void)hipStreamDestroy(side[i]);
+                side[i] = nullptr;
+            }
+        for (hipEvent_t& e : side_ev)
+            if (e) {
+                (void)hipEventDestroy(e);
+                e = nullptr;
+            }
         if (last_use) (void)hipEventDestroy(last_use);
         dbuf = ring_dev = ring_host = ring_host_dev = direct = nullptr;
         last_use = nullptr;
@@ -491,7 +506,8 @@ thread_local WorkspaceList tws;
 // pipeline streams it owned (those streams are destroyed with it).
 void drop_workspace(size_t i) {
     auto& l = tws.list;
-    const hipStream_t ps[2] = {l[i]->pipe_stream[0], l[i]->pipe_stream[1]};
+    const hipStream_t ps[2 + Workspace::kSideStreams] = {l[i]->pipe_stream[0], l[i]->pipe_stream[1], l[i]->side[0],
+                                                        l[i]->side[1], l[i]->side[2]};
     l.erase(l.begin() + i);
     for (hipStream_t p : ps)
         for (size_t j = 0; p && j < l.size();)
@@ -1301,6 +1317,12 @@ std::vector<HostRun> host_runs(const std::vector<P>& v, uint64_t bytes) {
 constexpr size_t kDirectMaxRuns = 16;                 // more runs: the gather / scatter ring
 constexpr uint64_t kDirectMaxBytes = 8ull << 30;      // device rows of one direct call
 constexpr uint64_t kDirectKeepBytes = 256ull << 20;   // direct rows kept for the next call (larger: freed)
+#ifndef LAMD_DIRECT_SLICES
+#define LAMD_DIRECT_SLICES 4
+#endif
+constexpr unsigned kDirectSlices = LAMD_DIRECT_SLICES;  // column slices of a direct call, one stream each (<= 4)
+static_assert(kDirectSlices >= 1 && kDirectSlices <= 4, "one stream per slice: the call's and three side streams");
+constexpr uint64_t kDirectSliceMinBytes = 4ull << 20;  // smaller calls: one slice
 
 // Host pieces that form a few row runs (the usual caller layout: pieces are
 // rows of one or a few arrays) go straight between the caller's pageable
@@ -1325,23 +1347,60 @@ LeopardResult run_host_direct(Call& c, uint64_t bytes, const std::vector<const u
     }
     uint8_t* din = ws.direct;
     uint8_t* dout = ws.direct + nin * bytes;
-    for (const HostRun& run : rin) {
-        uint8_t* dst = din + run.first * bytes;
-        if (run.stride == bytes)
-            HIP_OK(hipMemcpyAsync(dst, hin[run.first], run.count * bytes, hipMemcpyHostToDevice, c.s), "upload rows");
-        else
-            HIP_OK(hipMemcpy2DAsync(dst, bytes, hin[run.first], run.stride, bytes, run.count, hipMemcpyHostToDevice, c.s),
-                   "upload rows");
+    // Column slices, slice j on its own stream: upload, kernels, download.  One
+    // slice's upload then overlaps an earlier slice's kernels and download
+    // (PCIe carries both directions at once), where a single slice runs
+    // upload -> kernels -> download back to back.  The downloads are enqueued
+    // after every upload (a pageable download may hold the enqueueing thread).
+    const unsigned nsl = rows * bytes >= kDirectSliceMinBytes && bytes >= 4096 * kDirectSlices ? kDirectSlices : 1;
+    const uint64_t sw = nsl == 1 ? bytes : ((bytes + nsl - 1) / nsl + 63) / 64 * 64;  // slice width
+    std::vector<Call> cj(nsl, c);
+    if (nsl > 1) {
+        for (hipEvent_t& e : ws.side_ev)
+            if (!e) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
+        HIP_OK(hipEventRecord(ws.side_ev[0], c.s), "record direct rows");  // the rows' allocation and earlier work
+        for (unsigned j = 1; j < nsl; ++j) {
+            hipStream_t& st = ws.side[j - 1];
+            if (!st) HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "stream");
+            HIP_OK(hipStreamWaitEvent(st, ws.side_ev[0], 0), "order side stream");
+        }
     }
-    if ((r = fn(c, bytes, din, dout, bytes)) != Leopard_Success) return r;
-    HIP_OK(hipGetLastError(), "kernel launch");
-    for (const HostRun& run : rout) {
-        const uint8_t* src = dout + run.first * bytes;
-        if (run.stride == bytes)
-            HIP_OK(hipMemcpyAsync(hout[run.first], src, run.count * bytes, hipMemcpyDeviceToHost, c.s), "download rows");
-        else
-            HIP_OK(hipMemcpy2DAsync(hout[run.first], run.stride, src, bytes, bytes, run.count, hipMemcpyDeviceToHost, c.s),
-                   "download rows");
+    for (unsigned j = 0; j < nsl; ++j) {
+        if (j > 0) {
+            cj[j].s = ws.side[j - 1];
+            cj[j].ws = &workspace(c.dev, cj[j].s);  // scratch of its own (GF(2^16) intermediates)
+        }
+        const uint64_t o = uint64_t(j) * sw, len = std::min(sw, bytes - o);
+        for (const HostRun& run : rin) {
+            uint8_t* dst = din + run.first * bytes + o;
+            if (nsl == 1 && run.stride == bytes)
+                HIP_OK(hipMemcpyAsync(dst, hin[run.first], run.count * bytes, hipMemcpyHostToDevice, cj[j].s),
+                       "upload rows");
+            else
+                HIP_OK(hipMemcpy2DAsync(dst, bytes, hin[run.first] + o, run.stride, len, run.count,
+                                        hipMemcpyHostToDevice, cj[j].s),
+                       "upload rows");
+        }
+        if ((r = fn(cj[j], len, din + o, dout + o, bytes)) != Leopard_Success) return r;
+        HIP_OK(hipGetLastError(), "kernel launch");
+        if (j > 0 && (r = cj[j].ws->mark_use(cj[j].s)) != Leopard_Success) return r;
+    }
+    for (unsigned j = 0; j < nsl; ++j) {
+        const uint64_t o = uint64_t(j) * sw, len = std::min(sw, bytes - o);
+        for (const HostRun& run : rout) {
+            const uint8_t* src = dout + run.first * bytes + o;
+            if (nsl == 1 && run.stride == bytes)
+                HIP_OK(hipMemcpyAsync(hout[run.first], src, run.count * bytes, hipMemcpyDeviceToHost, cj[j].s),
+                       "download rows");
+            else
+                HIP_OK(hipMemcpy2DAsync(hout[run.first] + o, run.stride, src, bytes, len, run.count,
+                                        hipMemcpyDeviceToHost, cj[j].s),
+                       "download rows");
+        }
+    }
+    for (unsigned j = 1; j < nsl; ++j) {  // the call's stream waits for every slice
+        HIP_OK(hipEventRecord(ws.side_ev[j], cj[j].s), "record slice");
+        HIP_OK(hipStreamWaitEvent(c.s, ws.side_ev[j], 0), "join slice");
     }
     if (ws.direct_size > kDirectKeepBytes) {  // large rows do not stay with the thread: freed after this call's copies
         HIP_OK(hipFreeAsync(ws.direct, c.s), "free direct rows");

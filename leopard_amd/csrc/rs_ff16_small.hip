@@ -530,19 +530,27 @@ LDEV void dma_skew_set(uint32_t* set, const uint32_t* sktab, unsigned hi_fixed, 
 }
 // the multiply tables of log values logs[0, 256) (LDS), slot p = position p
 template <int NW>
-LDEV void dma_log_set(uint32_t* dst, const uint32_t* tabs, const uint32_t* logs, unsigned wave, unsigned lane) {
+LDEV void dma_log_set(uint32_t* dst, const uint32_t* tabs, const uint32_t* logs, unsigned wave, unsigned lane,
+                      bool sparse = false) {
+    // sparse: only the slots whose log value is not the zero table's (the
+    // reveal multiplies of the lost originals); the other slots keep stale
+    // bytes and are never read
     asm volatile("" : "+v"(lane));
     for (unsigned c = wave; c * 64u < kSetUnits; c += NW) {
         const unsigned u = c * 64u + lane;
         unsigned k;
         unsigned p = unit_slot(u, k);
         if (p == ~0u) p = 0u;
-        if (u < kSetUnits) dma16(tabs + size_t(logs[p]) * 24u + k * 4u, dst + c * 256u);
+        const uint32_t lg = logs[p];
+        if (u < kSetUnits && !(sparse && lg == FF16::kOrder)) dma16(tabs + size_t(lg) * 24u + k * 4u, dst + c * 256u);
     }
 }
 
 #ifndef LAMD_DEC16_ONE_DMA  // 1: stage the tables by LDS-DMA (A/B experiments; slower, see stage_tables)
 #define LAMD_DEC16_ONE_DMA 1
+#endif
+#ifndef LAMD_DEC16_ONE_EARLY  // 1: the next tile's skew set by DMA right after the IFFT (behind the fold)
+#define LAMD_DEC16_ONE_EARLY 1
 #endif
 #ifndef LAMD_DEC16_ONE_WAVES  // waves per SIMD the one-pass decoder's register budget is cut for
 #define LAMD_DEC16_ONE_WAVES 4
@@ -635,15 +643,17 @@ __global__ void __launch_bounds__((threads_n<8, R, LW>()), LAMD_DEC16_ONE_WAVES)
     // stores) at the tile boundaries, where the tile registers are free: the
     // 42 KB of one tile's tables land in ~0.5 us this way, against ~4 us for
     // LDS-DMA (which lands ~25 GB/s per CU, MI355X_MICROARCH.md ldsdma-fill).
-    auto stage_tables = [&](unsigned sk, const uint32_t* logs) {
+    // DMA: issued here, completed by tables_wait() (after the piece loads are
+    // issued too, so both are in flight together); register staging: done here
+    // (before the piece loads: its registers and the tile's are never live together)
+    auto stage_tables = [&](unsigned sk, const uint32_t* logs, bool sparse = false) {
 #if LAMD_DEC16_ONE_DMA
 #ifndef LAMD_X_NOSKEWDMA
         if (sk != ~0u) dma_skew_set<NW>(set, a.sktab, sk << T, wave, lane64);
 #endif
 #ifndef LAMD_X_NOLOGDMA
-        if (logs) dma_log_set<NW>(xch, a.tabs, logs, wave, lane64);
+        if (logs) dma_log_set<NW>(xch, a.tabs, logs, wave, lane64, sparse);
 #endif
-        wait_dma();
 #else
         Tabs16Stage<NT, T> st;
         LogTabs16Stage<NT, (1u << T)> ls;
@@ -651,7 +661,11 @@ __global__ void __launch_bounds__((threads_n<8, R, LW>()), LAMD_DEC16_ONE_WAVES)
         if (logs) ls.load(a.tabs, logs);
         if (sk != ~0u) st.store(set);
         if (logs) ls.store(xch);
+        (void)sparse;
 #endif
+    };
+    auto tables_wait = [&] {
+        if constexpr (LAMD_DEC16_ONE_DMA) wait_dma();
     };
     // first received tile: pieces, skew set, scale tables
     unsigned y = have ? unsigned(__builtin_ctz(have)) : a.nlo;
@@ -659,6 +673,7 @@ __global__ void __launch_bounds__((threads_n<8, R, LW>()), LAMD_DEC16_ONE_WAVES)
         stage_tables(y, slog + (y << T));
         __builtin_amdgcn_sched_barrier(0);
         load_tile(y, w0);
+        tables_wait();
         __syncthreads();
     }
     __builtin_amdgcn_sched_barrier(0);  // the accumulators start here, not across the first staging
@@ -681,6 +696,15 @@ __global__ void __launch_bounds__((threads_n<8, R, LW>()), LAMD_DEC16_ONE_WAVES)
             for (int k = 0; k < TL::U; ++k) asm volatile("" : "+v"(x[r][k]));
         }
         TL::ifft(x, w, lane, xch, PieceSpace{0, 0, y << T}, LdsWindow16{set, y << T, 0}, AllLive{});
+        // the next phase's skew set, by DMA, behind the fold (set is free once
+        // every wave is past the IFFT's last layer)
+        const unsigned rest0 = have & ~((2u << y) - 1u);
+        const unsigned ynext = rest0 ? unsigned(__builtin_ctz(rest0)) : a.nlo;
+        const unsigned sknext = ynext < a.nlo ? ynext : live ? a.tile0 + unsigned(__builtin_ctz(live)) : ~0u;
+        if constexpr (LAMD_DEC16_ONE_DMA && LAMD_DEC16_ONE_EARLY) {
+            __syncthreads();
+            if (sknext != ~0u) dma_skew_set<NW>(set, a.sktab, sknext << T, wave, lane64);
+        }
         STAMP1(2 + 3 * ti);
         asm volatile("" : "+v"(w));  // the fold's addresses: recomputed, not kept from the IFFT
         // fold U = x into the output tiles (every branch is workgroup-uniform)
@@ -716,19 +740,19 @@ __global__ void __launch_bounds__((threads_n<8, R, LW>()), LAMD_DEC16_ONE_WAVES)
         STAMP1(3 + 3 * ti);
         // next received tile (or the first output tile's skew set): its pieces,
         // tables by DMA, one wait
-        const unsigned rest = have & ~((2u << y) - 1u);
-        y = rest ? unsigned(__builtin_ctz(rest)) : a.nlo;
+        y = ynext;
         __syncthreads();  // every wave is done with set and xch
+        constexpr bool kSetDone = LAMD_DEC16_ONE_DMA && LAMD_DEC16_ONE_EARLY;  // set already on its way
         if (y < a.nlo) {
-            // tables first (L2-resident: a short wait), then the pieces, whose
-            // loads are in flight across the barrier: the staging registers
-            // and the tile registers are never live together
-            stage_tables(y, slog + (y << T));
+            // tables (L2-resident), then the pieces, whose loads are in flight
+            // across the barrier
+            stage_tables(kSetDone ? ~0u : y, slog + (y << T));
             __builtin_amdgcn_sched_barrier(0);
             load_tile(y, w);
-        } else if (live) {
+        } else if (live && !kSetDone) {
             stage_tables(a.tile0 + unsigned(__builtin_ctz(live)), nullptr);
         }
+        tables_wait();
         __syncthreads();
         STAMP1(4 + 3 * ti);
         ++ti;
@@ -743,12 +767,13 @@ __global__ void __launch_bounds__((threads_n<8, R, LW>()), LAMD_DEC16_ONE_WAVES)
         TL::fft(z[k], w, lane, xch, PieceSpace{0, 0, tk << T}, LdsWindow16{set, tk << T, 0}, AllLive{});
         __syncthreads();  // every wave is past the FFT's last exchange and its last table read
         const unsigned rest = live & ~((2u << k) - 1u);
-        stage_tables(rest ? a.tile0 + unsigned(__builtin_ctz(rest)) : ~0u, rlog + (k << 8));
+        stage_tables(rest ? a.tile0 + unsigned(__builtin_ctz(rest)) : ~0u, rlog + (k << 8), true);
         // lost original at p = m + i: work[i] = z[p] * exp(-el[p])  (LeopardFF16.cpp:1771-1773)
         auto pos = [&](int r) { return (tk << T) + TL::piece(0, r, w); };
         const uint32_t ew = a.erased_dev[(tk << 3) + (w >> (5 - R))];  // layout 0: one word a lane
         uint64_t po[TL::NR];
         lane_ptrs(po, a.out, [&](int r) { return pos(r) >= a.m ? min(pos(r) - a.m, a.K - 1) : 0u; });
+        tables_wait();
         __syncthreads();
         if (cl.live) {
 #pragma unroll

@@ -199,6 +199,17 @@ void release_device_memory(int dev, std::initializer_list<void*> ptrs) {
 // every call that used the workspace's memory -- is waited for before a
 // workspace is freed, so release is safe even after the caller destroyed the
 // stream.  (The reference holds no per-call state at all)
+// Events that only order work (a slot's reuse, a workspace's release, one
+// stream's wait for another): completion without the system-scope fence a
+// default event adds, which writes back and invalidates the caches and held
+// back the next kernel of a back-to-back stream by ~5.5 us (a decode call
+// marks its workspace use; profiles/r04_v13/ff8trace).  Events after which the
+// host reads what the device wrote keep the fence.
+#ifndef LAMD_ORDER_EVENT_FLAGS
+#define LAMD_ORDER_EVENT_FLAGS (hipEventDisableTiming | hipEventDisableSystemFence)
+#endif
+constexpr unsigned kOrderEvent = LAMD_ORDER_EVENT_FLAGS;
+
 struct Workspace {
     int dev = -1;
     hipStream_t stream = nullptr;
@@ -277,6 +288,19 @@ struct Workspace {
     std::vector<uint8_t> el8_valid;
     uint64_t el8_call = 0;
     unsigned el8_next = 0;
+    // Host copies of the slots (read back once per pattern, pinned): a single
+    // call whose pattern's locator is on the host passes it by value and reads
+    // no workspace memory, so it needs no completion marker after it (a marker
+    // between back-to-back kernels cost ~1.3 us a call, profiles/r04_v15).
+    // el8_state: 0 device only, 1 read-back pending (event el8_evi), 2 on the
+    // host.  el8_epoch tells a pending read-back of a slot's previous pattern
+    // from one of its current pattern.
+    static constexpr int kEl8Events = 4;
+    uint8_t* el8_host = nullptr;
+    std::vector<uint8_t> el8_state, el8_evi;
+    std::vector<uint32_t> el8_epoch;
+    hipEvent_t el8_ev[kEl8Events] = {};
+    std::vector<std::pair<unsigned, uint32_t>> el8_ev_slots[kEl8Events];  // (slot, epoch) per pending event
 
     ~Workspace() { release(); }
     // Waits for the work that may still use this workspace, then frees it.
@@ -293,6 +317,16 @@ struct Workspace {
             sl = StageSlot{};
         }
         release_device_memory(dev, {dbuf, ring_dev, direct, el8});
+        if (el8_host) (void)hipHostFree(el8_host);
+        el8_host = nullptr;
+        for (int e = 0; e < kEl8Events; ++e) {
+            if (el8_ev[e]) (void)hipEventDestroy(el8_ev[e]);
+            el8_ev[e] = nullptr;
+            el8_ev_slots[e].clear();
+        }
+        el8_state.clear();
+        el8_evi.clear();
+        el8_epoch.clear();
         for (Dec16Slot& d : dec16) {
             release_device_memory(dev, {d.mem});
             d = Dec16Slot{};
@@ -329,16 +363,22 @@ struct Workspace {
     // Called at the end of every call: marks where the work of this call that
     // uses the workspace's memory ends on the stream.
     LeopardResult mark_use(hipStream_t s) {
+#ifdef LAMD_X_NO_MARK  // A/B only: what the per-call event costs (unsafe release)
+        touched = false;
+#endif
         if (!touched) return Leopard_Success;
         touched = false;
-        if (!last_use) HIP_OK(hipEventCreateWithFlags(&last_use, hipEventDisableTiming), "event");
+        if (!last_use) HIP_OK(hipEventCreateWithFlags(&last_use, kOrderEvent), "event");
+#ifdef LAMD_X_TRACE_MARK
+        std::fprintf(stderr, "mark_use\n");
+#endif
         HIP_OK(hipEventRecord(last_use, s), "record workspace use");
         return Leopard_Success;
     }
     LeopardResult reserve_ring(size_t bytes_per_slot) {
         for (int s = 0; s < 2; ++s) {
             if (!pipe_stream[s]) HIP_OK(hipStreamCreateWithFlags(&pipe_stream[s], hipStreamNonBlocking), "stream");
-            if (!in_done[s]) HIP_OK(hipEventCreateWithFlags(&in_done[s], hipEventDisableTiming), "event");
+            if (!in_done[s]) HIP_OK(hipEventCreateWithFlags(&in_done[s], kOrderEvent), "event");
             if (!out_done[s]) HIP_OK(hipEventCreateWithFlags(&out_done[s], hipEventDisableTiming), "event");
         }
         if (bytes_per_slot <= slot_bytes) return Leopard_Success;
@@ -406,14 +446,21 @@ struct Workspace {
     // The device error locator of erasure bitmap `erased` (8 words): a cached
     // slot, or a new slot whose computation is appended to `jobs` (flush_el8
     // launches them, ahead of the decode kernels).
-    LeopardResult el8_slot(const uint32_t* erased, std::vector<El8Job>& jobs, const uint32_t** out) {
-        touched = true;
+    // The caller marks the workspace touched when a kernel reads the slot.
+    LeopardResult el8_slot(const uint32_t* erased, std::vector<El8Job>& jobs, const uint32_t** out,
+                           unsigned* slot_out = nullptr) {
         if (!el8) {
+            touched = true;
             HIP_OK(pool_alloc(reinterpret_cast<void**>(&el8), size_t(kEl8Slots) * 256, dev, stream),
                    "allocate error locators");
+            HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&el8_host), size_t(kEl8Slots) * 256, hipHostMallocDefault),
+                   "pinned error locators");
             el8_key.assign(kEl8Slots, El8Key{});
             el8_stamp.assign(kEl8Slots, 0);
             el8_valid.assign(kEl8Slots, 0);
+            el8_state.assign(kEl8Slots, 0);
+            el8_evi.assign(kEl8Slots, 0);
+            el8_epoch.assign(kEl8Slots, 0);
         }
         El8Key k;
         std::memcpy(k.e, erased, sizeof(k.e));
@@ -433,7 +480,10 @@ struct Workspace {
             if (el8_valid[slot]) el8_map.erase(el8_key[slot]);
             el8_key[slot] = k;
             el8_valid[slot] = 1;
+            el8_state[slot] = 0;
+            ++el8_epoch[slot];
             el8_map.emplace(k, slot);
+            touched = true;  // k_el8 writes the slot
             El8Job j;
             std::memcpy(j.erased, erased, sizeof(j.erased));
             j.slot = slot;
@@ -441,6 +491,47 @@ struct Workspace {
         }
         el8_stamp[slot] = el8_call;
         *out = el8 + size_t(slot) * 64;
+        if (slot_out) *slot_out = slot;
+        return Leopard_Success;
+    }
+    // The host copy of slot's locator, if it has arrived (never waits).
+    bool el8_value(unsigned slot, uint32_t* out) {
+        if (el8_state[slot] == 1) {
+            const int e = el8_evi[slot];
+            if (hipEventQuery(el8_ev[e]) != hipSuccess) return false;
+            for (const auto& se : el8_ev_slots[e])
+                if (el8_epoch[se.first] == se.second && el8_state[se.first] == 1) el8_state[se.first] = 2;
+            el8_ev_slots[e].clear();
+        }
+        if (el8_state[slot] != 2) return false;
+        std::memcpy(out, el8_host + size_t(slot) * 256, 256);
+        return true;
+    }
+    // Queues the read-back of slot's locator (after the work that writes it),
+    // if one of the read-back events is free.
+    LeopardResult el8_readback(unsigned slot, hipStream_t s) {
+        if (el8_state[slot] != 0) return Leopard_Success;
+        int e = -1;
+        for (int i = 0; i < kEl8Events && e < 0; ++i) {
+            if (!el8_ev[i]) {
+                // the host reads what the copy wrote: a default (system-fenced) event
+                HIP_OK(hipEventCreateWithFlags(&el8_ev[i], hipEventDisableTiming), "event");
+                e = i;
+            } else if (el8_ev_slots[i].empty() || hipEventQuery(el8_ev[i]) == hipSuccess) {
+                for (const auto& se : el8_ev_slots[i])
+                    if (el8_epoch[se.first] == se.second && el8_state[se.first] == 1) el8_state[se.first] = 2;
+                el8_ev_slots[i].clear();
+                e = i;
+            }
+        }
+        if (e < 0) return Leopard_Success;  // all busy: a later call of this pattern tries again
+        touched = true;
+        HIP_OK(hipMemcpyAsync(el8_host + size_t(slot) * 256, el8 + size_t(slot) * 64, 256, hipMemcpyDeviceToHost, s),
+               "read back error locator");
+        HIP_OK(hipEventRecord(el8_ev[e], s), "record read-back");
+        el8_ev_slots[e].emplace_back(slot, el8_epoch[slot]);
+        el8_state[slot] = 1;
+        el8_evi[slot] = uint8_t(e);
         return Leopard_Success;
     }
     // A slot whose computation failed to launch holds nothing valid.
@@ -473,7 +564,7 @@ struct Workspace {
             HIP_OK(hipEventSynchronize(sl.done), "wait staging slot");
             sl.pending = false;
         }
-        if (!sl.done) HIP_OK(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming), "event");
+        if (!sl.done) HIP_OK(hipEventCreateWithFlags(&sl.done, kOrderEvent), "event");
         if (bytes > sl.size) {
             if (sl.host) HIP_OK(hipHostFree(sl.host), "free staging");
             sl.host = nullptr;
@@ -957,13 +1048,29 @@ LeopardResult decode_device8(Call& c, uint64_t bytes, uint64_t off, unsigned K, 
     c.ws->el8_begin();
     std::vector<El8Job> jobs;
     const uint32_t* el = nullptr;
-    LeopardResult r = c.ws->el8_slot(erased, jobs, &el);
+    unsigned slot = 0;
+    LeopardResult r = c.ws->el8_slot(erased, jobs, &el, &slot);
     if (r != Leopard_Success) return r;
     if ((r = flush_el8(*c.ws, c.t, jobs, c.s)) != Leopard_Success) return r;
+    // the locator by value once the host holds it; until then the slot (and a
+    // read-back of it for the calls after this one)
+    uint32_t elv[kFf8Ptrs / 4];
+    const bool by_value = c.ws->el8_value(slot, elv);
+#ifdef LAMD_X_TRACE_MARK
+    std::fprintf(stderr, "el8 slot %u state %d by_value %d\n", slot, int(c.ws->el8_state[slot]), int(by_value));
+#endif
+    if (!by_value) {
+        c.ws->touched = true;
+        if ((r = c.ws->el8_readback(slot, c.s)) != Leopard_Success) return r;
+    }
     Ff8DecArgs a;
     for (uint64_t pos = 0; pos < bytes; pos += kFf8MaxLaunchBytes) {  // see encode_device
         const int mode =
             fill_dec8(a, c.t, K, R, orig, rec, work, off + pos, std::min(kFf8MaxLaunchBytes, bytes - pos), el);
+        if (by_value) {
+            std::memcpy(a.el_val, elv, sizeof(elv));
+            a.el_by_value = 1;
+        }
         HIP_OK(mode == kDec8General ? launch_ff8_decode(Tn, a, c.s)
                : mode == kDec8Split ? launch_ff8_decode_split(Tn - 1, a, c.s)
                                     : launch_ff8_decode_half(Tn - 1, a, c.s),
@@ -1317,10 +1424,15 @@ std::vector<HostRun> host_runs(const std::vector<P>& v, uint64_t bytes) {
 constexpr size_t kDirectMaxRuns = 16;                 // more runs: the gather / scatter ring
 constexpr uint64_t kDirectMaxBytes = 8ull << 30;      // device rows of one direct call
 constexpr uint64_t kDirectKeepBytes = 256ull << 20;   // direct rows kept for the next call (larger: freed)
+// Column slices of a direct call, one stream each (<= 4).  Measured on the
+// pageable 128+128 x 64 KiB encode: 4 slices 16.1-16.6 GB/s, 1 slice 22.4-22.5
+// (512+512: 22.3-22.5 vs 24.2-24.5, profiles/r04_v9/host.txt): the strided 2-D
+// copies of a slice move less per SDMA command than one whole-row copy, and the
+// copy engines, not the overlap, bound the call.  One slice stays the default.
 #ifndef LAMD_DIRECT_SLICES
-#define LAMD_DIRECT_SLICES 4
+#define LAMD_DIRECT_SLICES 1
 #endif
-constexpr unsigned kDirectSlices = LAMD_DIRECT_SLICES;  // column slices of a direct call, one stream each (<= 4)
+constexpr unsigned kDirectSlices = LAMD_DIRECT_SLICES;
 static_assert(kDirectSlices >= 1 && kDirectSlices <= 4, "one stream per slice: the call's and three side streams");
 constexpr uint64_t kDirectSliceMinBytes = 4ull << 20;  // smaller calls: one slice
 
@@ -1357,7 +1469,7 @@ LeopardResult run_host_direct(Call& c, uint64_t bytes, const std::vector<const u
     std::vector<Call> cj(nsl, c);
     if (nsl > 1) {
         for (hipEvent_t& e : ws.side_ev)
-            if (!e) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
+            if (!e) HIP_OK(hipEventCreateWithFlags(&e, kOrderEvent), "event");
         HIP_OK(hipEventRecord(ws.side_ev[0], c.s), "record direct rows");  // the rows' allocation and earlier work
         for (unsigned j = 1; j < nsl; ++j) {
             hipStream_t& st = ws.side[j - 1];
@@ -2216,6 +2328,7 @@ LeopardResult decode_batch(unsigned count, uint64_t bytes, unsigned K, unsigned 
                     },
                     [&](Call& c) -> LeopardResult {  // the error locators of the new patterns, one launch
                         c.ws->el8_begin();
+                        c.ws->touched = true;  // the batch's kernels read the slots
                         std::vector<El8Job> jobs;
                         for (unsigned o = 0; o < nb; ++o) {
                             uint32_t erased[8];

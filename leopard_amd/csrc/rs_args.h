@@ -104,6 +104,8 @@ struct Ff8DecArgs {
     uint32_t present[kPyr8Words];  // pyramid of received positions (Pyr8Live)
     uint32_t needed[kPyr8Words];   // pyramid of lost originals
     const uint32_t* el;            // error locator of this pattern, one byte per position (k_el8's output)
+    uint32_t el_val[kFf8Ptrs / 4]; // the same bytes by value (el_by_value): a single call whose pattern's
+    uint32_t el_by_value;          //   locator the host already holds reads no workspace memory
     const uint32_t* sktab;
     const uint32_t* tabs;          // multiply tables by log value; entry 256 is all zero
     const uint32_t* fused;         // k_ff8_dec_half: fused top-layer table of this m (= encoder chunk 0's)

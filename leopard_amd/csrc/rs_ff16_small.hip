@@ -93,6 +93,7 @@ LDEV void st_unit(uint8_t* piece, uint64_t off, const uint32_t* x) {
     *gptr<uint32_t>(piece + off + 32) = x[1];
 }
 
+constexpr int lg2(unsigned v) { return v <= 1 ? 0 : 1 + lg2(v >> 1); }
 constexpr int lg_bits(int LW) { return LW == 64 ? 0 : LW == 32 ? 1 : LW == 16 ? 2 : 3; }
 template <int T, int R, int LW>
 constexpr unsigned threads_n() { return 64u << (T - R - lg_bits(LW)); }
@@ -528,37 +529,69 @@ LDEV void dma_skew_set(uint32_t* set, const uint32_t* sktab, unsigned hi_fixed, 
         if (u < kSetUnits) dma16(sktab + size_t(hi_fixed + sl - 1u) * 24u + k * 4u, set + c * 256u);
     }
 }
-// the multiply tables of log values logs[0, 256) (LDS), slot p = position p
+// the multiply tables of log values logs[0, 256) (global memory), slot p =
+// position p.  The log values of all of this wave's units are read first and
+// the DMAs issued after them: the wait for a log value then covers only the log
+// reads (vmcnt retires in order), not DMAs issued before this call.
+// sparse: only the slots whose log value is not the zero table's (the reveal
+// multiplies of the lost originals); the other slots keep stale bytes and are
+// never read.
 template <int NW>
 LDEV void dma_log_set(uint32_t* dst, const uint32_t* tabs, const uint32_t* logs, unsigned wave, unsigned lane,
                       bool sparse = false) {
-    // sparse: only the slots whose log value is not the zero table's (the
-    // reveal multiplies of the lost originals); the other slots keep stale
-    // bytes and are never read
+    constexpr unsigned kChunks = (kSetUnits + 63) / 64, kPer = (kChunks + NW - 1) / NW;
     asm volatile("" : "+v"(lane));
-    for (unsigned c = wave; c * 64u < kSetUnits; c += NW) {
-        const unsigned u = c * 64u + lane;
+    uint32_t lg[kPer];
+#pragma unroll
+    for (unsigned i = 0; i < kPer; ++i) {
+        const unsigned u = (wave + i * NW) * 64u + lane;
         unsigned k;
-        unsigned p = unit_slot(u, k);
+        unsigned p = unit_slot(u < kSetUnits ? u : 0u, k);
         if (p == ~0u) p = 0u;
-        const uint32_t lg = logs[p];
-        if (u < kSetUnits && !(sparse && lg == FF16::kOrder)) dma16(tabs + size_t(lg) * 24u + k * 4u, dst + c * 256u);
+        lg[i] = logs[p];
+    }
+    asm volatile("" : "+v"(lane));  // the unit -> slot arithmetic redone below, not kept live
+    // every source address before the first DMA: a wait for a log value after a
+    // DMA has been issued would wait for that DMA too
+    const uint32_t* src[kPer];
+    bool go[kPer];
+#pragma unroll
+    for (unsigned i = 0; i < kPer; ++i) {
+        const unsigned c = wave + i * NW, u = c * 64u + lane;
+        unsigned k;
+        unit_slot(u < kSetUnits ? u : 0u, k);
+        src[i] = tabs + size_t(lg[i]) * 24u + k * 4u;
+        go[i] = u < kSetUnits && !(sparse && lg[i] == FF16::kOrder);
+        asm volatile("" : "+v"(src[i]));
+    }
+#pragma unroll
+    for (unsigned i = 0; i < kPer; ++i) {
+        const unsigned c = wave + i * NW;
+        if (c < kChunks && go[i]) dma16(src[i], dst + c * 256u);
     }
 }
+// 4 bytes per lane from src (per lane) to dst + 4 * lane (dst wave-uniform)
+LDEV void dma4(const uint32_t* src, uint32_t* dst) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src),
+                                     (__attribute__((address_space(3))) void*)(dst), 4, 0, 0);
+#endif
+}
 
-#ifndef LAMD_DEC16_ONE_DMA  // 1: stage the tables by LDS-DMA (A/B experiments; slower, see stage_tables)
-#define LAMD_DEC16_ONE_DMA 1
-#endif
-#ifndef LAMD_DEC16_ONE_EARLY  // 1: the next tile's skew set by DMA right after the IFFT (behind the fold)
-#define LAMD_DEC16_ONE_EARLY 1
-#endif
 #ifndef LAMD_DEC16_ONE_WAVES  // waves per SIMD the one-pass decoder's register budget is cut for
 #define LAMD_DEC16_ONE_WAVES 4
 #endif
+// LDS of the one-pass decoder (dwords): the exchange area (transposes; the image
+// of the next received tile's pieces between them; the reveal tables), the skew
+// set, the scale tables, the next tile's piece addresses
 template <int R, int LW>
 constexpr size_t one_xch_dwords() {
     constexpr size_t x = Tile<FF16, 8, R, 1, LW, 0, lg_bits(LW)>::kXchDwords;
     return x > tab16_slot(256) ? x : tab16_slot(256);
+}
+template <int R, int LW>
+constexpr size_t one_lds_dwords() {
+    return one_xch_dwords<R, LW>() + 2 * tab16_set_dwords(8) + 2 * 256;
 }
 template <int R, int LW, int NZ>
 __global__ void __launch_bounds__((threads_n<8, R, LW>()), LAMD_DEC16_ONE_WAVES) k_dec16n_one(DecArgs a) {
@@ -567,20 +600,16 @@ __global__ void __launch_bounds__((threads_n<8, R, LW>()), LAMD_DEC16_ONE_WAVES)
     using TL = Tile<FF16, T, R, 1, LW, 0, G>;
     constexpr unsigned NT = threads_n<T, R, LW>(), NW = NT / 64;
     constexpr size_t kSet = tab16_set_dwords(T);
-    // the exchange area also holds a tile's scale / reveal tables between its
-    // transforms: at narrow strips (LW = 8) it is sized for those
     constexpr size_t kXch = one_xch_dwords<R, LW>();
+    static_assert(LW <= 32 && TL::U == 2, "a DMA lane's unit half is the same in every instruction");
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    uint32_t* xch = lds;         // transposes; the scale / reveal tables between them
-    uint32_t* set = lds + kXch;  // skew tables of the current tile
-    uint32_t* slog = set + kSet;           // scale log values of the received tiles (256 a tile)
-    uint32_t* rlog = slog + 8 * 256;       // reveal log values of the output tiles
+    uint32_t* xch = lds;                 // transposes; the next tile's piece image; the reveal tables
+    uint32_t* set = lds + kXch;          // skew tables of the current transform
+    uint32_t* stab = set + kSet;         // scale tables of the current received tile
+    uint64_t* ptab = reinterpret_cast<uint64_t*>(stab + kSet);  // piece addresses of the next received tile
     const unsigned wave = uniform(threadIdx.x >> 6), lane64 = threadIdx.x & 63u, lane = threadIdx.x & (LW - 1);
     const unsigned w0 = (wave << G) | (lane64 >> (6 - G));
-    // 64-byte strips: the two halves of a 128-byte line on one XCD (workgroups
-    // are dealt round-robin over the 8 XCDs: b and b + 8 share one)
-    const unsigned nb = gridDim.x, b = blockIdx.x;
-    const uint64_t strip = (LW < 16 && (nb & 7u) == 0) ? (b & 7u) * (nb >> 3) + (b >> 3) : b;
+    const uint64_t strip = blockIdx.x;
     const NarrowCols<LW> cl = narrow_cols<LW>(a.nunits, lane, strip);
 #ifdef LAMD_STAMPS  // 32 stamps per wave: 0 start, 1 first tile staged, per input tile i 2+3i (scale + IFFT), 3+3i (fold), 4+3i (next tile's wait), 26+k output tile k done
 #define STAMP1(k)                                                                                              \
@@ -604,76 +633,85 @@ __global__ void __launch_bounds__((threads_n<8, R, LW>()), LAMD_DEC16_ONE_WAVES)
     unsigned have = 0;
     for (unsigned y = 0; y < a.nlo; ++y)
         if (pyr_bit(a.present_pyr, T, y)) have |= 1u << y;
-    // prologue: the log values of the scale and reveal multiplies into LDS
-    for (unsigned i = threadIdx.x; i < a.nlo * 256u; i += NT) slog[i] = a.scale_logs[i];
-    for (unsigned i = threadIdx.x; i < unsigned(NZ) * 256u; i += NT)
-        if ((live >> (i >> 8)) & 1u) rlog[i] = a.reveal_logs[((a.tile0 + (i >> 8)) << 8) + (i & 255u)];
-    __syncthreads();
+    auto next_have = [&](unsigned y) {  // first received tile after y (a.nlo: none)
+        const unsigned rest = have & ~((2u << y) - 1u);
+        return rest ? unsigned(__builtin_ctz(rest)) : a.nlo;
+    };
 
-    typename TL::Reg z[NZ], x;
-    // received pieces of tile y: positions [0, R) recovery, [m, m + K)
-    // originals (LeopardFF16.cpp:1715-1730); absent ones read the zero page
-    auto load_tile = [&](unsigned y, unsigned w) {
-        const uint32_t ew = a.erased_dev[(y << 3) + (w >> (5 - R))];
-#pragma unroll
-        for (int r = 0; r < TL::NR; ++r) {
-            const unsigned tp = TL::piece(0, r, w), p = (y << T) + tp;
+    // Received pieces of tile yt: positions [0, R) recovery, [m, m + K)
+    // originals (LeopardFF16.cpp:1715-1730); 0 = absent (read the zero page).
+    // (Addressing slab maps directly in front of each DMA instead, a scalar
+    // erasure-word load and a 64-bit multiply per instruction, measured slower:
+    // 1000+200 x 64 KiB decode 190 vs 164 us, profiles/r04_v10.)
+    auto build_ptab = [&](unsigned yt) {
+        for (unsigned tp = threadIdx.x; tp < 256u; tp += NT) {
+            const unsigned p = (yt << T) + tp;
             const bool is_rec = p < a.R, is_orig = p >= a.m && p < a.m + a.K;
-            const bool got = !((ew >> (tp & 31)) & 1u) && (is_rec || is_orig);
             const PieceMap& pm = is_rec ? a.rec : a.orig;
             const unsigned idx = is_rec ? p : (is_orig ? p - a.m : 0u);
-            const uint8_t* src = got ? (pm.table ? reinterpret_cast<const uint8_t*>(pm.table[idx])
-                                                 : pm.base + uint64_t(idx) * pm.stride) + pm.off
-                                     : a.zeros;
-            ld_unit(x[r], src, got ? cl.off : (cl.off & 31));
+            // both loads issued before either is used (one latency, not two)
+            const uint32_t ew = a.erased_dev[(yt << 3) + (tp >> 5)];
+            const uint64_t b = pm.table ? pm.table[idx] : uint64_t(reinterpret_cast<uintptr_t>(pm.base)) + uint64_t(idx) * pm.stride;
+            const bool got = !((ew >> (tp & 31u)) & 1u) && (is_rec || is_orig);
+            ptab[tp] = got ? b + pm.off : 0ull;
         }
     };
-#ifdef LAMD_DEC16_ONE_STAGGER
-    // experiment: the second round of workgroups (most likely the second one on
-    // each CU) starts LAMD_DEC16_ONE_STAGGER x 0.1 us late, so the two
-    // workgroups of a CU do not reach their load waits together
-    if (blockIdx.x >= gridDim.x / 2) {
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (__builtin_amdgcn_s_memrealtime() - t0 < uint64_t(LAMD_DEC16_ONE_STAGGER) * 10u) __builtin_amdgcn_s_sleep(8);
-    }
-#endif
-    // the tables of the next phase into LDS: the skew set of tile `sk` (if
-    // sk != ~0u) into set, the multiply tables of log values logs[0, 256) (if
-    // logs) into xch.  Staged through registers (global loads, then LDS
-    // stores) at the tile boundaries, where the tile registers are free: the
-    // 42 KB of one tile's tables land in ~0.5 us this way, against ~4 us for
-    // LDS-DMA (which lands ~25 GB/s per CU, MI355X_MICROARCH.md ldsdma-fill).
-    // DMA: issued here, completed by tables_wait() (after the piece loads are
-    // issued too, so both are in flight together); register staging: done here
-    // (before the piece loads: its registers and the tile's are never live together)
-    auto stage_tables = [&](unsigned sk, const uint32_t* logs, bool sparse = false) {
-#if LAMD_DEC16_ONE_DMA
-#ifndef LAMD_X_NOSKEWDMA
-        if (sk != ~0u) dma_skew_set<NW>(set, a.sktab, sk << T, wave, lane64);
-#endif
-#ifndef LAMD_X_NOLOGDMA
-        if (logs) dma_log_set<NW>(xch, a.tabs, logs, wave, lane64, sparse);
-#endif
-#else
-        Tabs16Stage<NT, T> st;
-        LogTabs16Stage<NT, (1u << T)> ls;
-        if (sk != ~0u) st.load(a.sktab, -1, sk << T, 0);
-        if (logs) ls.load(a.tabs, logs);
-        if (sk != ~0u) st.store(set);
-        if (logs) ls.store(xch);
-        (void)sparse;
-#endif
+    // The pieces of the tile in ptab into xch by 16-byte LDS-DMA.  Each wave
+    // fetches exactly what its own lanes hold in layout 0 (tile pieces
+    // r | vw << R of its virtual waves vw = 4 wave + g), so a wave's own vmcnt
+    // covers its reads.  Instruction q of wave W fills 1 KiB: 16-byte slot
+    // i = 32 rho + 16 h + 4 g + k' holds chunk k = (k' & 1) | 2 h | (k' >> 1) << 2
+    // (16 bytes: the low (h = 0) or high (h = 1) bytes of 4 units) of tile piece
+    // (2 q + rho) | (4 W + g) << R.  A read of one register's low (or high)
+    // dwords then touches 16 distinct 16-byte bank groups: conflict-free.
+    static_assert(LW == 16 && R == 3 && G == 2, "16-unit strips, 8 pieces a lane, 4 lane groups");
+    auto dma_pieces = [&] {
+        // lanes of a strip without its second 64-byte block (a last strip of 8
+        // units) re-read the first block; those units are never stored
+        const bool one_block = strip * LW + 8u >= a.nunits;
+        const uint64_t sbase = uint64_t(unit_offset<FF16>(strip * LW));
+        unsigned ln = lane64;
+        asm volatile("" : "+v"(ln));
+        const unsigned rho = ln >> 5, h = (ln >> 4) & 1u, g = (ln >> 2) & 3u, kp = ln & 3u;
+        unsigned k = (kp & 1u) | (h << 1) | ((kp >> 1) << 2);
+        if (one_block) k &= 3u;
+#pragma unroll
+        for (unsigned q = 0; q < 4; ++q) {
+            const uint64_t base = ptab[(2u * q + rho) | ((wave * 4u + g) << R)];
+            const uint8_t* src = base ? reinterpret_cast<const uint8_t*>(base) + sbase + 16u * k : a.zeros + 16u * (k & 3u);
+            dma16(reinterpret_cast<const uint32_t*>(src), xch + (wave * 4u + q) * 256u);
+        }
     };
-    auto tables_wait = [&] {
-        if constexpr (LAMD_DEC16_ONE_DMA) wait_dma();
+    auto read_pieces = [&](typename TL::Reg& x, unsigned w) {
+        (void)w;
+        const unsigned g = (lane64 >> 4) & 3u, l = lane64 & 15u;
+        const unsigned kp = ((l >> 2) & 1u) | ((l >> 3) << 1);
+        const uint32_t* base = xch + wave * 1024u + (g * 4u + kp) * 4u + (l & 3u);
+#pragma unroll
+        for (int r = 0; r < TL::NR; ++r) {
+            const uint32_t* p = base + (r >> 1) * 256 + (r & 1) * 128;
+            x[r][0] = p[0];   // h = 0
+            x[r][1] = p[64];  // h = 1: 16 slots on
+        }
     };
-    // first received tile: pieces, skew set, scale tables
+
+    typename TL::Reg z[NZ], x;
+    // first received tile: piece image, skew set and scale tables, one wait
     unsigned y = have ? unsigned(__builtin_ctz(have)) : a.nlo;
     if (y < a.nlo) {
-        stage_tables(y, slog + (y << T));
-        __builtin_amdgcn_sched_barrier(0);
-        load_tile(y, w0);
-        tables_wait();
+        build_ptab(y);
+        __syncthreads();
+        dma_log_set<NW>(stab, a.tabs, a.scale_logs + (y << T), wave, lane64);
+        dma_skew_set<NW>(set, a.sktab, y << T, wave, lane64);
+        dma_pieces();
+        wait_dma();
+        __syncthreads();
+        read_pieces(x, w0);
+        const unsigned yn = next_have(y);
+        if (yn < a.nlo) build_ptab(yn);  // (every wave's DMAs are issued: ptab is free)
+    } else if (live) {
+        dma_skew_set<NW>(set, a.sktab, (a.tile0 + unsigned(__builtin_ctz(live))) << T, wave, lane64);
+        wait_dma();
         __syncthreads();
     }
     __builtin_amdgcn_sched_barrier(0);  // the accumulators start here, not across the first staging
@@ -690,35 +728,42 @@ __global__ void __launch_bounds__((threads_n<8, R, LW>()), LAMD_DEC16_ONE_WAVES)
 #pragma unroll
         for (int r = 0; r < TL::NR; ++r) {
             asm volatile("" ::: "memory");  // one table live at a time
-            const FF16::Tab t = FF16::tab_lds(xch + tab16_slot(TL::piece(0, r, w)));
+            const FF16::Tab t = FF16::tab_lds(stab + tab16_slot(TL::piece(0, r, w)));
             FF16::mul(x[r], x[r], t);
 #pragma unroll
             for (int k = 0; k < TL::U; ++k) asm volatile("" : "+v"(x[r][k]));
         }
         TL::ifft(x, w, lane, xch, PieceSpace{0, 0, y << T}, LdsWindow16{set, y << T, 0}, AllLive{});
-        // the next phase's skew set, by DMA, behind the fold (set is free once
-        // every wave is past the IFFT's last layer)
-        const unsigned rest0 = have & ~((2u << y) - 1u);
-        const unsigned ynext = rest0 ? unsigned(__builtin_ctz(rest0)) : a.nlo;
+        const unsigned ynext = next_have(y);
         const unsigned sknext = ynext < a.nlo ? ynext : live ? a.tile0 + unsigned(__builtin_ctz(live)) : ~0u;
-        if constexpr (LAMD_DEC16_ONE_DMA && LAMD_DEC16_ONE_EARLY) {
-            __syncthreads();
-            if (sknext != ~0u) dma_skew_set<NW>(set, a.sktab, sknext << T, wave, lane64);
-        }
         STAMP1(2 + 3 * ti);
+        // every wave is past the IFFT: set, stab and xch are free.  The next
+        // phase's tables go out now, its pieces once the derivative is done with
+        // xch; all of them land during the fold.
+        __syncthreads();
+        if (ynext < a.nlo) dma_log_set<NW>(stab, a.tabs, a.scale_logs + (ynext << T), wave, lane64);
+        if (sknext != ~0u) dma_skew_set<NW>(set, a.sktab, sknext << T, wave, lane64);
         asm volatile("" : "+v"(w));  // the fold's addresses: recomputed, not kept from the IFFT
-        // fold U = x into the output tiles (every branch is workgroup-uniform)
+        // the formal derivative's low bits: D_lo U_t for t = y (rs_device.h derivative_add)
         static_for<0, NZ>([&](auto K) {
             constexpr int k = decltype(K)::value;
-            if (!((live >> k) & 1u)) return;
-            const unsigned t = a.tile0 + k;
-            if (t == y) {  // the formal derivative's low bits: D_lo U_t (rs_device.h derivative_add)
+            if (((live >> k) & 1u) && a.tile0 + k == y) {
                 unsigned wd = w;
                 asm volatile("" : "+v"(wd));
                 TL::derivative_add(z[k], [&](int r, uint32_t* out) { out[0] = x[r][0]; out[1] = x[r][1]; }, wd, lane,
                                    xch);
-                return;
             }
+        });
+        if (ynext < a.nlo) {
+            __syncthreads();  // every wave is done with xch
+            dma_pieces();
+        }
+        // fold U = x into the other output tiles (every branch is workgroup-uniform)
+        static_for<0, NZ>([&](auto K) {
+            constexpr int k = decltype(K)::value;
+            if (!((live >> k) & 1u)) return;
+            const unsigned t = a.tile0 + k;
+            if (t == y) return;
             const uint32_t q = cload(a.qlog + (t ^ y));
             if (q == kQZero) return;
             if (q == kQOne) {
@@ -738,22 +783,15 @@ __global__ void __launch_bounds__((threads_n<8, R, LW>()), LAMD_DEC16_ONE_WAVES)
             }
         });
         STAMP1(3 + 3 * ti);
-        // next received tile (or the first output tile's skew set): its pieces,
-        // tables by DMA, one wait
+        // next received tile: its pieces, scale tables and skew set have landed
         y = ynext;
-        __syncthreads();  // every wave is done with set and xch
-        constexpr bool kSetDone = LAMD_DEC16_ONE_DMA && LAMD_DEC16_ONE_EARLY;  // set already on its way
-        if (y < a.nlo) {
-            // tables (L2-resident), then the pieces, whose loads are in flight
-            // across the barrier
-            stage_tables(kSetDone ? ~0u : y, slog + (y << T));
-            __builtin_amdgcn_sched_barrier(0);
-            load_tile(y, w);
-        } else if (live && !kSetDone) {
-            stage_tables(a.tile0 + unsigned(__builtin_ctz(live)), nullptr);
-        }
-        tables_wait();
+        wait_dma();
         __syncthreads();
+        if (y < a.nlo) {
+            read_pieces(x, w);
+            const unsigned yn = next_have(y);
+            if (yn < a.nlo) build_ptab(yn);  // visible to the DMAs after the IFFT's barriers
+        }
         STAMP1(4 + 3 * ti);
         ++ti;
     }
@@ -764,16 +802,22 @@ __global__ void __launch_bounds__((threads_n<8, R, LW>()), LAMD_DEC16_ONE_WAVES)
         const unsigned tk = a.tile0 + k;
         unsigned w = w0;  // opaque per output tile, as in the tile loop
         asm volatile("" : "+v"(w));
+        // the reveal tables of the lost originals (the others are never read),
+        // landing during the FFT (stab is free once every wave is past the
+        // previous reveal)
+        __syncthreads();
+        dma_log_set<NW>(stab, a.tabs, a.reveal_logs + (tk << T), wave, lane64, true);
         TL::fft(z[k], w, lane, xch, PieceSpace{0, 0, tk << T}, LdsWindow16{set, tk << T, 0}, AllLive{});
         __syncthreads();  // every wave is past the FFT's last exchange and its last table read
+        // the next output tile's skew set
         const unsigned rest = live & ~((2u << k) - 1u);
-        stage_tables(rest ? a.tile0 + unsigned(__builtin_ctz(rest)) : ~0u, rlog + (k << 8), true);
+        if (rest) dma_skew_set<NW>(set, a.sktab, (a.tile0 + unsigned(__builtin_ctz(rest))) << T, wave, lane64);
         // lost original at p = m + i: work[i] = z[p] * exp(-el[p])  (LeopardFF16.cpp:1771-1773)
         auto pos = [&](int r) { return (tk << T) + TL::piece(0, r, w); };
         const uint32_t ew = a.erased_dev[(tk << 3) + (w >> (5 - R))];  // layout 0: one word a lane
         uint64_t po[TL::NR];
         lane_ptrs(po, a.out, [&](int r) { return pos(r) >= a.m ? min(pos(r) - a.m, a.K - 1) : 0u; });
-        tables_wait();
+        wait_dma();
         __syncthreads();
         if (cl.live) {
 #pragma unroll
@@ -782,7 +826,7 @@ __global__ void __launch_bounds__((threads_n<8, R, LW>()), LAMD_DEC16_ONE_WAVES)
                 if (p >= a.m && p < a.m + a.K && ((ew >> (tp & 31)) & 1u)) {
                     asm volatile("" ::: "memory");
                     uint32_t o[2];
-                    FF16::mul(o, z[k][r], FF16::tab_lds(xch + tab16_slot(tp)));
+                    FF16::mul(o, z[k][r], FF16::tab_lds(stab + tab16_slot(tp)));
                     st_unit(reinterpret_cast<uint8_t*>(po[r]), cl.off, o);
                 }
             }
@@ -827,12 +871,9 @@ constexpr int kDecOneR = LAMD_DEC16_ONE_R;
 #ifndef LAMD_DEC16_ONE_LW
 #define LAMD_DEC16_ONE_LW 16
 #endif
-// 64-byte strips (one ALTMAP block of every piece), 4-wave workgroups of
-// 8 positions a lane (Z: 64 VGPRs): three workgroups per CU (168 VGPRs, 48 KB
-// of LDS each)
 constexpr int kDecOneLW = LAMD_DEC16_ONE_LW;
-constexpr size_t kDecOneLds = (one_xch_dwords<kDecOneR, kDecOneLW>() + tab16_set_dwords(8) + 8 * 256 + kDecOneNZ * 256) * 4;
-static_assert(kDecOneLW != 8 || kDecOneLds <= 160 * 1024 / 3, "three workgroups per CU");
+constexpr size_t kDecOneLds = one_lds_dwords<kDecOneR, kDecOneLW>() * 4;
+static_assert(kDecOneLds <= 160 * 1024 / 2, "two workgroups per CU");
 }  // namespace
 
 #ifdef LAMD_STAMPS
@@ -879,8 +920,8 @@ hipError_t launch_decode16_small_lo(const DecArgs& a, hipStream_t s) {
     return launch16n(&k_dec16n_lo<kDecR, kDecLW>, dim3(strips, a.nlo), threads_n<8, kDecR, kDecLW>(), kDecLds, a, s);
 }
 // one-pass form: at most kDecOneNZ output tiles
-#ifndef LAMD_DEC16_ONE  // 0: the two-pass form only (A/B experiments)
-#define LAMD_DEC16_ONE 0
+#ifndef LAMD_DEC16_ONE  // 0: the two-pass form only (A/B builds)
+#define LAMD_DEC16_ONE 1
 #endif
 bool decode16_one_supported(unsigned nout) { return LAMD_DEC16_ONE && nout <= unsigned(kDecOneNZ); }
 hipError_t launch_decode16_one(const DecArgs& a, hipStream_t s) {

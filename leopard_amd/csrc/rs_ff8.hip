@@ -395,8 +395,7 @@ __global__ void __launch_bounds__(threads_for(T, RB), LAMD_SLAB_WAVES) k_ff8_enc
 // layers across lanes (__shfl_xor) and two in registers.  Fully reduced mod 255
 // (the reference reduces partially, 255 standing for 0: the same residues; the
 // multiply tables of log 0 and log 255 are the same, x * exp(0) = x * exp(255)).
-// The decode kernels then copy the 256 el bytes into LDS in their prologue
-// (ElLoad8): one dword load per lane of wave 0, issued ahead of the piece loads.
+// The decode kernels read it at their top (ElRegs).
 struct Mod8 {
     LDEV static unsigned add(unsigned a, unsigned b) { const unsigned s = a + b; return s >= 255u ? s - 255u : s; }
     LDEV static unsigned sub(unsigned a, unsigned b) { const unsigned s = a + 255u - b; return s >= 255u ? s - 255u : s; }
@@ -433,14 +432,29 @@ __global__ void __launch_bounds__(64) k_el8(El8Args a) {
     fwht256_mod255(e, lane);
     a.out[size_t(job.slot) * 64 + lane] = e[0] | (e[1] << 8) | (e[2] << 16) | (e[3] << 24);
 }
-// The error locator of this launch's pattern (k_el8's output) into LDS.
-struct ElLoad8 {
-    uint32_t v;
-    LDEV void load(const Ff8DecArgs& a, unsigned wave, unsigned lane) {
-        if (wave == 0) v = *gptr<const uint32_t>(a.el + lane);
+// The error locator of this launch's pattern (k_el8's output, one byte per
+// position) at a wave-uniform position, through the scalar cache: from the
+// argument block when the host passes it by value, else from the workspace slot
+// (an LDS copy put an LDS round trip in front of every scale table read).
+LDEV uint32_t el_word(const Ff8DecArgs& a, unsigned i) { return a.el_by_value ? a.el_val[i] : cload(a.el + i); }
+// The el bytes of a lane's NR layout-0 positions p0 + r (p0 = w << R: NR
+// consecutive positions, wave-uniform), read at the top of the kernel so that
+// their latency (kernel-argument or scalar-cache reads) overlaps the piece loads
+// instead of sitting in front of the first scale multiply.
+// (p0 is a multiple of NR: NR < 4 positions share one word.)
+template <int NR>
+struct ElRegs {
+    static constexpr int kW = NR >= 4 ? NR / 4 : 1;
+    uint32_t wd[kW];
+    unsigned off;
+    LDEV void load(const Ff8DecArgs& a, unsigned p0) {
+        off = p0 & 3u;
+#pragma unroll
+        for (int i = 0; i < kW; ++i) wd[i] = el_word(a, (p0 >> 2) + i);
     }
-    LDEV void store(uint8_t* el, unsigned wave, unsigned lane) const {
-        if (wave == 0) reinterpret_cast<uint32_t*>(el)[lane] = v;
+    LDEV unsigned at(int r) const {
+        const unsigned q = off + unsigned(r);
+        return (wd[q >> 2] >> ((q & 3u) * 8u)) & 0xFFu;
     }
 };
 
@@ -469,20 +483,18 @@ LDEV void ff8_dec(const Ff8DecArgs& a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const LdsTab8<256> sk{lds + areas8(NA) * tile_dwords_for(T, RB)};
     const LdsTab8<256> ltab{sk.base + LdsTab8<256>::kDwords};  // by log value
-    uint8_t* el = reinterpret_cast<uint8_t*>(ltab.base + LdsTab8<256>::kDwords);
     LdsRing<tile_dwords_for(T, RB), areas8(NA)> ring{lds};
     STAMP(0);
     TabStage8<threads_for(T, RB), 256> sk_stage, log_stage;
     sk_stage.load(a.sktab);
     log_stage.load(a.tabs);
     const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    ElLoad8 elc;
-    elc.load(a, w, lane);
     const Cols cl = strip_cols(a.nunits, lane);
     const PieceSpace ps{0, 0, 0};
     const Pyr8Live present{a.present}, needed{a.needed};
     auto pos = [&](int r) { return TL::piece(0, r, w); };
-    auto el_at = [&](unsigned p) { return unsigned(el[p]); };
+    ElRegs<TL::NR> el;
+    el.load(a, pos(0));
     typename TL::Reg v;
     {
         // received pieces: positions [0, R) recovery, [m, m + K) originals (LeopardFF8.cpp:1857-1877)
@@ -492,13 +504,12 @@ LDEV void ff8_dec(const Ff8DecArgs& a) {
         for (int r = 0; r < TL::NR; ++r) v[r][0] = present(pos(r), 0) ? gload(pp[r], cl) : 0u;
     }
     STAMP(1);
-    elc.store(el, w, lane);
     sk_stage.store(sk);
     log_stage.store(ltab);
     __syncthreads();
     STAMP(2);
     // scale by exp(el) (absent pieces stay zero)
-    scale_batched<TL>(v, ltab, [&](int r) { return el_at(pos(r)); }, [&](int r) { return present(pos(r), 0); });
+    scale_batched<TL>(v, ltab, [&](int r) { return el.at(r); }, [&](int r) { return present(pos(r), 0); });
     // decoder skew base -1 (LeopardFF8.cpp:1880, 1903), piece space {0, 0, 0}
     const LdsSkew8Fixed<-1> win{{{sk}}};
     // IFFT and FFT without their top layers around swap_top + D_low (see
@@ -522,7 +533,7 @@ LDEV void ff8_dec(const Ff8DecArgs& a) {
     uint64_t pp[TL::NR];
     fetch_ptrs(pp, a, pos);
     auto is_needed = [&](int r) { return needed(pos(r), 0); };
-    scale_batched<TL>(v, ltab, [&](int r) { return F::kModulus - el_at(pos(r)); }, is_needed);
+    scale_batched<TL>(v, ltab, [&](int r) { return F::kModulus - el.at(r); }, is_needed);
     if (!cl.live) return;
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r)
@@ -561,14 +572,10 @@ LDEV void ff8_dec_half(const Ff8DecArgs& a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const LdsTab8<256> sk{lds + tile_dwords_for(T, RB)};
     const LdsTab8<256> ltab{sk.base + LdsTab8<256>::kDwords};  // by log value
-    uint8_t* el = reinterpret_cast<uint8_t*>(ltab.base + LdsTab8<256>::kDwords);
-    auto el_at = [&](unsigned p) { return unsigned(el[p]); };
     TabStage8<threads_for(T, RB), 256> sk_stage, log_stage;
     sk_stage.load(a.sktab);
     log_stage.load(a.tabs);
     const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    ElLoad8 elc;
-    elc.load(a, w, lane);
     const Cols cl = strip_cols(a.nunits, lane);
     const PieceSpace low{0, 0, 0}, high{0, 0, m};
     auto pyr = [](const uint32_t* w) {
@@ -578,6 +585,9 @@ LDEV void ff8_dec_half(const Ff8DecArgs& a) {
     const auto present = pyr(a.present), needed = pyr(a.needed);
     auto lpos = [&](int r) { return TL::piece(0, r, w); };
     auto hpos = [&](int r) { return m + TL::piece(0, r, w); };
+    ElRegs<TL::NR> el_lo, el_hi;
+    el_lo.load(a, lpos(0));
+    el_hi.load(a, hpos(0));
     typename TL::Reg v;
     {
         uint64_t pp[TL::NR];
@@ -585,11 +595,10 @@ LDEV void ff8_dec_half(const Ff8DecArgs& a) {
 #pragma unroll
         for (int r = 0; r < TL::NR; ++r) v[r][0] = present(lpos(r), 0) ? gload(pp[r], cl) : 0u;
     }
-    elc.store(el, w, lane);
     sk_stage.store(sk);
     log_stage.store(ltab);
     __syncthreads();
-    scale_batched<TL>(v, ltab, [&](int r) { return el_at(lpos(r)); }, [&](int r) { return present(lpos(r), 0); });
+    scale_batched<TL>(v, ltab, [&](int r) { return el_lo.at(r); }, [&](int r) { return present(lpos(r), 0); });
     Skew8Win win{{sk}};
     win.stage(nullptr, -1);  // decoder skew base (LeopardFF8.cpp:1880, 1903)
     // both top layers (single skews m/2 - 1 and m + m/2 - 1) as one butterfly
@@ -601,7 +610,7 @@ LDEV void ff8_dec_half(const Ff8DecArgs& a) {
     uint64_t pp[TL::NR];
     fetch_ptrs(pp, a, hpos);
     auto is_needed = [&](int r) { return needed(hpos(r), 0); };
-    scale_batched<TL>(v, ltab, [&](int r) { return F::kModulus - el_at(hpos(r)); }, is_needed);
+    scale_batched<TL>(v, ltab, [&](int r) { return F::kModulus - el_hi.at(r); }, is_needed);
     if (!cl.live) return;
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r)
@@ -637,19 +646,18 @@ LDEV void ff8_dec_split(const Ff8DecArgs& a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const LdsTab8<256> sk{lds + tile_dwords_for(T, RB)};
     const LdsTab8<256> ltab{sk.base + LdsTab8<256>::kDwords};  // by log value
-    uint8_t* el = reinterpret_cast<uint8_t*>(ltab.base + LdsTab8<256>::kDwords);
-    auto el_at = [&](unsigned p) { return unsigned(el[p]); };
     TabStage8<threads_for(T, RB), 256> sk_stage, log_stage;
     sk_stage.load(a.sktab);
     log_stage.load(a.tabs);
     const unsigned w = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    ElLoad8 elc;
-    elc.load(a, w, lane);
     const Cols cl = strip_cols(a.nunits, lane);
     const PieceSpace low{0, 0, 0}, high{0, 0, m};
     const Pyr8Live present{a.present}, needed{a.needed};
     auto lpos = [&](int r) { return TL::piece(0, r, w); };
     auto hpos = [&](int r) { return m + TL::piece(0, r, w); };
+    ElRegs<TL::NR> el_lo, el_hi;
+    el_lo.load(a, lpos(0));
+    el_hi.load(a, hpos(0));
     typename TL::Reg x, h;
     {
         uint64_t pp[TL::NR];
@@ -660,20 +668,19 @@ LDEV void ff8_dec_split(const Ff8DecArgs& a) {
 #pragma unroll
         for (int r = 0; r < TL::NR; ++r) x[r][0] = present(lpos(r), 0) ? gload(pp[r], cl) : 0u;
     }
-    elc.store(el, w, lane);
     sk_stage.store(sk);
     log_stage.store(ltab);
     __syncthreads();
     Skew8Win win{{sk}};
     win.stage(nullptr, -1);  // decoder skew base (LeopardFF8.cpp:1880, 1903)
     // y = N(I_H(h * exp(el)))
-    scale_batched<TL>(h, ltab, [&](int r) { return el_at(hpos(r)); }, [&](int r) { return present(hpos(r), 0); });
+    scale_batched<TL>(h, ltab, [&](int r) { return el_hi.at(r); }, [&](int r) { return present(hpos(r), 0); });
     TL::template ifft<false>(h, w, lane, lds, high, win, present);
     typename TL::Reg y;
     TL::zero(y);
     TL::derivative_add(y, [&](int r, uint32_t* out) { out[0] = h[r][0]; }, w, lane, lds);
     // x <- I_L(x * exp(el)) ^ y, then F_H
-    scale_batched<TL>(x, ltab, [&](int r) { return el_at(lpos(r)); }, [&](int r) { return present(lpos(r), 0); });
+    scale_batched<TL>(x, ltab, [&](int r) { return el_lo.at(r); }, [&](int r) { return present(lpos(r), 0); });
     TL::template ifft<false>(x, w, lane, lds, low, LdsSkew8Fixed<-1>{{{sk}}}, present);
     TL::xor_into(x, y);
     TL::template fft<false>(x, w, lane, lds, high, win, needed);
@@ -681,7 +688,7 @@ LDEV void ff8_dec_split(const Ff8DecArgs& a) {
     uint64_t pp[TL::NR];
     fetch_ptrs(pp, a, hpos);
     auto is_needed = [&](int r) { return needed(hpos(r), 0); };
-    scale_batched<TL>(x, ltab, [&](int r) { return F::kModulus - el_at(hpos(r)); }, is_needed);
+    scale_batched<TL>(x, ltab, [&](int r) { return F::kModulus - el_hi.at(r); }, is_needed);
     if (!cl.live) return;
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r)

@@ -23,3 +23,6 @@ PMC_TOOL=shape_time KB_ARGS="$SH" bash tools/pmc.sh \
   FETCH_SIZE WRITE_SIZE || exit 1
 python3 tools/pmc_summary.py gpurun_out/pmc1 gpurun_out/pmc2 gpurun_out/pmc3 gpurun_out/pmc4 > $OUT/pmc_summary.txt
 python3 tools/pmc_derive.py $OUT/pmc_summary.txt | tee $OUT/pmc_derived.txt
+python3 tools/pmc_traffic.py $(echo $SH | cut -d, -f1-3 | tr , " ") gpurun_out/pmc3 gpurun_out/pmc4 > $OUT/pmc_traffic_${SH%%,*}x$(echo $SH | cut -d, -f2).json
+cat $OUT/pmc_traffic_*.json
+rm -rf gpurun_out/pmc1 gpurun_out/pmc2 gpurun_out/pmc3 gpurun_out/pmc4  # raw passes: summarised above

@@ -19,3 +19,4 @@ python3 tools/pmc_traffic.py ${PMC_ARGS:-128 128 65536} gpurun_out/pmc1 gpurun_o
 rm -rf gpurun_out/pmc1 gpurun_out/pmc2
 PMC_TOOL=bbench KB_ARGS="${PMC_ARGS:-128 128 65536} 16" bash tools/pmc.sh FETCH_SIZE WRITE_SIZE || exit 1
 python3 tools/pmc_traffic.py --objects 16 ${PMC_ARGS:-128 128 65536} gpurun_out/pmc1 gpurun_out/pmc2 > $OUT/pmc_traffic_batch.json && cat $OUT/pmc_traffic_batch.json
+rm -rf gpurun_out/pmc1 gpurun_out/pmc2 $OUT/prof  # raw passes and traces: summarised above

@@ -98,7 +98,60 @@ constexpr int lg_bits(int LW) { return LW == 64 ? 0 : LW == 32 ? 1 : LW == 16 ? 
 template <int T, int R, int LW>
 constexpr unsigned threads_n() { return 64u << (T - R - lg_bits(LW)); }
 
+// ------------------------------------------------------------- LDS-DMA --
+
+// 16 bytes per lane from src (per lane) to dst + 16 * lane (dst wave-uniform)
+LDEV void dma16(const uint32_t* src, uint32_t* dst) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src),
+                                     (__attribute__((address_space(3))) void*)(dst), 16, 0, 0);
+#endif
+}
+LDEV void wait_dma() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// 16-byte unit u of a table set laid out by tab16_slot (slot s at 5 s + (s >> 3)
+// + (s >> 6) units): its slot and its unit inside the slot, or slot ~0u for a
+// padding unit.
+LDEV unsigned unit_slot(unsigned u, unsigned& k) {
+    const unsigned b = u / 329u, r = u - b * 329u;
+    const unsigned g = r / 41u, r2 = r - g * 41u;
+    if (r == 328u || r2 == 40u) {
+        k = 0;
+        return ~0u;
+    }
+    const unsigned i = r2 / 5u;
+    k = r2 - i * 5u;
+    return 64u * b + 8u * g + i;
+}
+constexpr unsigned kSetUnits = unsigned(tab16_set_dwords(8) / 4);  // = tab16_slot(256) / 4
+static_assert(tab16_slot(256) / 4 == kSetUnits, "skew and log sets have the same footprint");
+// The skew set of entries base + s, slot s in [1, 2^T) (Tabs16Stage::load(sktab,
+// base, 0, 0)'s entries) by LDS-DMA.  (lane is made opaque: the unit -> slot
+// arithmetic is redone at each use instead of being hoisted out of the tile
+// loops and kept live.)
+template <int NW, int T>
+LDEV void dma_skew_set_at(uint32_t* set, const uint32_t* sktab, int base, unsigned wave, unsigned lane) {
+    constexpr unsigned kUnits = unsigned(tab16_set_dwords(T) / 4);
+    asm volatile("" : "+v"(lane));
+    for (unsigned c = wave; c * 64u < kUnits; c += NW) {
+        const unsigned u = c * 64u + lane;
+        unsigned k;
+        unsigned sl = unit_slot(u, k);
+        if (sl == ~0u || sl == 0u || sl >= (1u << T)) sl = 1u;  // padding and the unused slot 0: any valid entry
+        if (u < kUnits) dma16(sktab + size_t(int64_t(base) + sl) * 24u + k * 4u, set + c * 256u);
+    }
+}
+// skew set of tile hi_fixed >> 8 at skew base -1 (the decoder's)
+template <int NW>
+LDEV void dma_skew_set(uint32_t* set, const uint32_t* sktab, unsigned hi_fixed, unsigned wave, unsigned lane) {
+    dma_skew_set_at<NW, 8>(set, sktab, int(hi_fixed) - 1, wave, lane);
+}
+
 // ------------------------------------------------------------------ encode --
+
+#ifndef LAMD_ENC16N_DMA  // 1: the next stage's skew set by LDS-DMA during the current chunk's IFFT (measured slower: 54.7 vs 52.3 us at 1000+200 x 64 KiB, r04_v19)
+#define LAMD_ENC16N_DMA 0
+#endif
+constexpr bool kEncDma = LAMD_ENC16N_DMA;
 
 template <int T, int R, int LW>
 LDEV void enc16n_body(const EncArgs& a) {
@@ -156,6 +209,13 @@ LDEV void enc16n_body(const EncArgs& a) {
         const bool more = c + 1 < a.nchunks;
         if (more)  // next chunk's pieces in flight during this chunk's transform
             load_chunk(nx, c + 1, [] {});
+        if constexpr (kEncDma) {
+            // the next stage's skew set (chunk c + 1's IFFT, or the FFT's) by LDS-DMA
+            // into the set chunk c - 1 used (every wave is past that IFFT: the
+            // barrier above), landing during this chunk's IFFT
+            dma_skew_set_at<int(NT / 64), T>(set_of(c + 1), a.sktab, more ? int(m - 1 + (c + 1) * m) : -1, wave,
+                                             threadIdx.x & 63u);
+        }
         // an opaque copy of w per chunk: the per-lane table addresses are
         // recomputed in each chunk instead of being hoisted and kept live
         unsigned wc = w;
@@ -166,7 +226,7 @@ LDEV void enc16n_body(const EncArgs& a) {
         STAMP16(2 + (c < 3 ? c : 3));
         if (!more) break;
         ++c;
-        {
+        if constexpr (!kEncDma) {
             // its tables (L2-resident after the first workgroups: a short wait),
             // into the set chunk c - 2 used (read before the previous barrier)
             Tabs16Stage<NT, T> st;
@@ -174,14 +234,19 @@ LDEV void enc16n_body(const EncArgs& a) {
             st.store(set_of(c));
         }
         take_chunk(x, nx, c);
+        if constexpr (kEncDma) wait_dma();
         __syncthreads();
     }
     {
         // FFT tables (skew base -1) into the set the last chunk did not use
         uint32_t* fset = set_of(a.nchunks);
-        Tabs16Stage<NT, T> st;
-        st.load(a.sktab, -1, 0, 0);
-        st.store(fset);
+        if constexpr (kEncDma) {
+            wait_dma();
+        } else {
+            Tabs16Stage<NT, T> st;
+            st.load(a.sktab, -1, 0, 0);
+            st.store(fset);
+        }
         __syncthreads();
         TL::template fft<true>(acc, w, lane, lds, ps, LdsWindow16Static<-1, 0>{{fset, 0, 0}}, AllLive{});
     }
@@ -491,44 +556,6 @@ LDEV void dec16n_fin_body(const DecArgs& a) {
 // Each tile boundary is one exposed wait (the DMA of the next tables and the
 // next pieces' loads); two workgroups per CU cover each other's.
 
-// 16 bytes per lane from src (per lane) to dst + 16 * lane (dst wave-uniform)
-LDEV void dma16(const uint32_t* src, uint32_t* dst) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src),
-                                     (__attribute__((address_space(3))) void*)(dst), 16, 0, 0);
-#endif
-}
-LDEV void wait_dma() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-// 16-byte unit u of a table set laid out by tab16_slot (slot s at 5 s + (s >> 3)
-// + (s >> 6) units): its slot and its unit inside the slot, or slot ~0u for a
-// padding unit.
-LDEV unsigned unit_slot(unsigned u, unsigned& k) {
-    const unsigned b = u / 329u, r = u - b * 329u;
-    const unsigned g = r / 41u, r2 = r - g * 41u;
-    if (r == 328u || r2 == 40u) {
-        k = 0;
-        return ~0u;
-    }
-    const unsigned i = r2 / 5u;
-    k = r2 - i * 5u;
-    return 64u * b + 8u * g + i;
-}
-constexpr unsigned kSetUnits = unsigned(tab16_set_dwords(8) / 4);  // = tab16_slot(256) / 4
-static_assert(tab16_slot(256) / 4 == kSetUnits, "skew and log sets have the same footprint");
-// skew set of tile hi_fixed >> 8 at skew base -1 (Tabs16Stage's entries)
-// (lane is made opaque: the unit -> slot arithmetic is redone at each use
-// instead of being hoisted out of the tile loops and kept live)
-template <int NW>
-LDEV void dma_skew_set(uint32_t* set, const uint32_t* sktab, unsigned hi_fixed, unsigned wave, unsigned lane) {
-    asm volatile("" : "+v"(lane));
-    for (unsigned c = wave; c * 64u < kSetUnits; c += NW) {
-        const unsigned u = c * 64u + lane;
-        unsigned k;
-        unsigned sl = unit_slot(u, k);
-        if (sl == ~0u || sl == 0u) sl = 1u;  // padding and the unused slot 0: any valid entry
-        if (u < kSetUnits) dma16(sktab + size_t(hi_fixed + sl - 1u) * 24u + k * 4u, set + c * 256u);
-    }
-}
 // the multiply tables of log values logs[0, 256) (global memory), slot p =
 // position p.  The log values of all of this wave's units are read first and
 // the DMAs issued after them: the wait for a log value then covers only the log
@@ -741,6 +768,8 @@ __global__ void __launch_bounds__((threads_n<8, R, LW>()), LAMD_DEC16_ONE_WAVES)
         // phase's tables go out now, its pieces once the derivative is done with
         // xch; all of them land during the fold.
         __syncthreads();
+        // (Staging them through registers at the tile boundary instead spills 22
+        // VGPRs next to the accumulators.)
         if (ynext < a.nlo) dma_log_set<NW>(stab, a.tabs, a.scale_logs + (ynext << T), wave, lane64);
         if (sknext != ~0u) dma_skew_set<NW>(set, a.sktab, sknext << T, wave, lane64);
         asm volatile("" : "+v"(w));  // the fold's addresses: recomputed, not kept from the IFFT

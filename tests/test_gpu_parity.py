@@ -121,6 +121,46 @@ def test_decode_roundtrip_and_oracle(leo, k, r, b, loss):
         assert np.array_equal(got[i], expect[i]), i
 
 
+# The single-pass GF(2^16) decoder (k_dec16n_one: n <= 2048, <= 4 tiles of originals,
+# pieces >= 32 KiB): a tile mixing recovery and original positions (m = 128), a last
+# column strip of 8 units (B = 64 mod 128), lost recovery pieces, every original lost,
+# and callers' pointer tables (pieces scattered over the rows of a store).
+@pytest.mark.parametrize("k,r,b,loss,layout", [(300, 100, 33344, 60, "slab"), (1000, 200, 32832, 150, "scattered"),
+                                               (500, 500, 32768, 500, "slab")])
+def test_single_pass_ff16_decoder_matches_oracle(leo, k, r, b, loss, layout):
+    rng = np.random.default_rng(k + r + loss)
+    data = rng.integers(0, 256, (k, b), dtype=np.uint8)
+    junk = rng.integers(0, 256, (r, b), dtype=np.uint8)  # not a codeword: the exact decoder map is compared
+    lost_o = sorted(rng.choice(k, loss, replace=False).tolist())
+    lost_r = sorted(rng.choice(r, r - loss, replace=False).tolist())
+    expect = ol.oracle().decode(data, junk, lost_o, lost_r)
+    wc = leo.leo_decode_work_count(k, r)
+    if layout == "slab":
+        orig, rec = dev_tensor(data), dev_tensor(junk)
+        work = torch.zeros((wc, b), dtype=torch.uint8, device="cuda")
+        po = [orig[i].data_ptr() for i in range(k)]
+        pr = [rec[i].data_ptr() for i in range(r)]
+        pw = [work[i].data_ptr() for i in range(wc)]
+        row = {i: i for i in range(wc)}
+    else:
+        perm_o, perm_r, perm_w = rng.permutation(k), rng.permutation(r), rng.permutation(wc)
+        orig = dev_tensor(data[np.argsort(perm_o)])  # piece i at row perm_o[i]
+        rec = dev_tensor(junk[np.argsort(perm_r)])
+        work = torch.zeros((wc, b), dtype=torch.uint8, device="cuda")
+        po = [orig[int(perm_o[i])].data_ptr() for i in range(k)]
+        pr = [rec[int(perm_r[i])].data_ptr() for i in range(r)]
+        pw = [work[int(perm_w[i])].data_ptr() for i in range(wc)]
+        row = {i: int(perm_w[i]) for i in range(wc)}
+    lo, lr = set(lost_o), set(lost_r)
+    res = leo.leo_decode(b, k, r, wc, [None if i in lo else po[i] for i in range(k)],
+                         [None if i in lr else pr[i] for i in range(r)], pw)
+    assert res == leo.LeopardResult.Success, leo.last_error()
+    torch.cuda.synchronize()
+    got = work.cpu().numpy()
+    for i in lost_o:
+        assert np.array_equal(got[row[i]], expect[i]), i
+
+
 @pytest.mark.parametrize("key", _golden_keys("decout_"))
 def test_decode_matches_reference_golden(leo, key):
     k, r, b, loss = (int(x) for x in key.split("_")[1:])

@@ -669,7 +669,7 @@ def kernels_for(k, r, nbytes, loss):
     enc = ("k_enc16n" if narrow and m in (128, 256) else
            "k_enc_fused" if m <= 256 and not (m == 256 and k > m and nbytes < 512 << 10) else "k_enc_lo + k_enc_hi + k_enc_fin")
     nout = ((m + k - 1) >> 8) - (m >> 8) + 1  # 256-position tiles holding originals
-    dec = (("k_dec16n_one" if nbytes >= 32 << 10 and nout <= 4 else "k_dec16n_lo + k_dec16n_fin") if narrow and n <= 2048 else
+    dec = (("k_dec16n_one" if nbytes >= 60 << 10 and nout <= 4 else "k_dec16n_lo + k_dec16n_fin") if narrow and n <= 2048 else
            "k_el16 (new pattern) + k_dec_lo + k_dec_hi%s + k_dec_fin" % ("_half" if loss == k and 2 * m == n else ""))
     return {"encode": enc, "decode": dec}
 

@@ -718,7 +718,7 @@ struct MapBuilder {
 // Pieces of at most this many bytes count as narrow columns for the small
 // GF(2^16) kernels (rs_ff16_small.hip): 256 KiB = 2048 strips of 128 bytes.
 constexpr uint64_t kNarrowColumnsMax = 256 << 10;
-constexpr uint64_t kOnePassMinBytes = 32 << 10;
+constexpr uint64_t kOnePassMinBytes = 60 << 10;  // the single-pass GF(2^16) decoder from here (rs_ff16_small.hip)
 
 // Columns per GF(2^8) launch: its argument block counts dword columns in 32 bits.
 constexpr uint64_t kFf8MaxLaunchBytes = 1ull << 32;

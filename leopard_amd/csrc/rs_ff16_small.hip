@@ -685,35 +685,37 @@ __global__ void __launch_bounds__((threads_n<8, R, LW>()), LAMD_DEC16_ONE_WAVES)
     };
     // The pieces of the tile in ptab into xch by 16-byte LDS-DMA.  Each wave
     // fetches exactly what its own lanes hold in layout 0 (tile pieces
-    // r | vw << R of its virtual waves vw = 4 wave + g), so a wave's own vmcnt
-    // covers its reads.  Instruction q of wave W fills 1 KiB: 16-byte slot
-    // i = 32 rho + 16 h + 4 g + k' holds chunk k = (k' & 1) | 2 h | (k' >> 1) << 2
-    // (16 bytes: the low (h = 0) or high (h = 1) bytes of 4 units) of tile piece
-    // (2 q + rho) | (4 W + g) << R.  A read of one register's low (or high)
-    // dwords then touches 16 distinct 16-byte bank groups: conflict-free.
-    static_assert(LW == 16 && R == 3 && G == 2, "16-unit strips, 8 pieces a lane, 4 lane groups");
+    // r | vw << R of its NG virtual waves vw = NG wave + g), so a wave's own
+    // vmcnt covers its reads.  Instruction q of wave W fills 1 KiB: 16-byte slot
+    // i = 32 rho + 16 h + KP g + k' holds chunk k = 4 (k' >> 1) + (k' & 1) + 2 h
+    // (16 bytes: the low (h = 0) or high (h = 1) bytes of 4 units of 64-byte
+    // block k' >> 1) of tile piece (2 q + rho) | (NG W + g) << R.  A read of one
+    // register's low (or high) dwords then touches 16 distinct 16-byte bank
+    // groups: conflict-free.
+    constexpr unsigned NG = 64u / LW, KP = LW / 4u;  // lane groups; low-byte chunks of a strip
+    static_assert((LW == 16 || LW == 32) && R == 3 && NG * KP == 16, "16- or 32-unit strips, 8 pieces a lane");
     auto dma_pieces = [&] {
-        // lanes of a strip without its second 64-byte block (a last strip of 8
-        // units) re-read the first block; those units are never stored
-        const bool one_block = strip * LW + 8u >= a.nunits;
+        // a last strip of fewer 64-byte blocks re-reads its last block for the
+        // missing ones; those units are never stored
+        const unsigned nblk = unsigned(min(uint64_t(LW / 8u), (a.nunits - strip * LW) / 8u));
         const uint64_t sbase = uint64_t(unit_offset<FF16>(strip * LW));
         unsigned ln = lane64;
         asm volatile("" : "+v"(ln));
-        const unsigned rho = ln >> 5, h = (ln >> 4) & 1u, g = (ln >> 2) & 3u, kp = ln & 3u;
-        unsigned k = (kp & 1u) | (h << 1) | ((kp >> 1) << 2);
-        if (one_block) k &= 3u;
+        const unsigned rho = ln >> 5, h = (ln >> 4) & 1u, g = (ln & 15u) / KP, kp = (ln & 15u) % KP;
+        const unsigned blk = min(kp >> 1, nblk - 1u);
+        const unsigned k = 4u * blk + (kp & 1u) + 2u * h;
 #pragma unroll
         for (unsigned q = 0; q < 4; ++q) {
-            const uint64_t base = ptab[(2u * q + rho) | ((wave * 4u + g) << R)];
-            const uint8_t* src = base ? reinterpret_cast<const uint8_t*>(base) + sbase + 16u * k : a.zeros + 16u * (k & 3u);
+            const uint64_t base = ptab[(2u * q + rho) | ((wave * NG + g) << R)];
+            const uint8_t* src = base ? reinterpret_cast<const uint8_t*>(base) + sbase + 16u * k : a.zeros + 16u * k;
             dma16(reinterpret_cast<const uint32_t*>(src), xch + (wave * 4u + q) * 256u);
         }
     };
     auto read_pieces = [&](typename TL::Reg& x, unsigned w) {
         (void)w;
-        const unsigned g = (lane64 >> 4) & 3u, l = lane64 & 15u;
-        const unsigned kp = ((l >> 2) & 1u) | ((l >> 3) << 1);
-        const uint32_t* base = xch + wave * 1024u + (g * 4u + kp) * 4u + (l & 3u);
+        const unsigned g = lane64 / LW, l = lane64 % LW;
+        const unsigned kp = 2u * (l >> 3) + ((l >> 2) & 1u);
+        const uint32_t* base = xch + wave * 1024u + (g * KP + kp) * 4u + (l & 3u);
 #pragma unroll
         for (int r = 0; r < TL::NR; ++r) {
             const uint32_t* p = base + (r >> 1) * 256 + (r & 1) * 128;
@@ -897,12 +899,18 @@ constexpr int kDecOneNZ = 4;  // output tiles held per lane by the one-pass deco
 #define LAMD_DEC16_ONE_R 3
 #endif
 constexpr int kDecOneR = LAMD_DEC16_ONE_R;
-#ifndef LAMD_DEC16_ONE_LW
-#define LAMD_DEC16_ONE_LW 16
-#endif
-constexpr int kDecOneLW = LAMD_DEC16_ONE_LW;
-constexpr size_t kDecOneLds = one_lds_dwords<kDecOneR, kDecOneLW>() * 4;
-static_assert(kDecOneLds <= 160 * 1024 / 2, "two workgroups per CU");
+// Column strips of 16 units (128 bytes, 8-wave workgroups, two per CU) or 32
+// units (16-wave workgroups, one per CU: each tile's tables are staged once per
+// CU instead of twice).  32 is taken when it makes one full round of 240..256
+// workgroups (60-64 KiB pieces): 1000+200 x 64 KiB 150.6 vs 156.8-157.1 us,
+// 600+400 133.1 vs 139.6; at 128 KiB (two rounds) the two are equal
+// (profiles/r04_v21, r04_v22).  The host takes the one-pass form only from
+// 60 KiB pieces (fewer workgroups leave SIMDs idle: at 32 KiB it ran 96.7 us
+// against 87.2 for the two passes, at 48 KiB 145.8 against 139.7, at 56 KiB
+// 148.6 against 147.1; r04_v22, r04_v23).
+constexpr size_t kDecOneLds16 = one_lds_dwords<kDecOneR, 16>() * 4;
+constexpr size_t kDecOneLds32 = one_lds_dwords<kDecOneR, 32>() * 4;
+static_assert(kDecOneLds16 <= 160 * 1024 / 2 && kDecOneLds32 <= 160 * 1024, "two / one workgroup(s) per CU");
 }  // namespace
 
 #ifdef LAMD_STAMPS
@@ -954,9 +962,13 @@ hipError_t launch_decode16_small_lo(const DecArgs& a, hipStream_t s) {
 #endif
 bool decode16_one_supported(unsigned nout) { return LAMD_DEC16_ONE && nout <= unsigned(kDecOneNZ); }
 hipError_t launch_decode16_one(const DecArgs& a, hipStream_t s) {
-    const unsigned strips = unsigned((a.nunits + kDecOneLW - 1) / kDecOneLW);
-    return launch16n(&k_dec16n_one<kDecOneR, kDecOneLW, kDecOneNZ>, dim3(strips), threads_n<8, kDecOneR, kDecOneLW>(),
-                     kDecOneLds, a, s);
+    const unsigned strips32 = unsigned((a.nunits + 31) / 32);
+    if (strips32 >= 240 && strips32 <= 256)
+        return launch16n(&k_dec16n_one<kDecOneR, 32, kDecOneNZ>, dim3(strips32), threads_n<8, kDecOneR, 32>(),
+                         kDecOneLds32, a, s);
+    const unsigned strips = unsigned((a.nunits + 15) / 16);
+    return launch16n(&k_dec16n_one<kDecOneR, 16, kDecOneNZ>, dim3(strips), threads_n<8, kDecOneR, 16>(), kDecOneLds16,
+                     a, s);
 }
 // both passes over `count` objects of one shape (same nlo, nout, column count)
 hipError_t launch_decode16_small_batch(const DecArgs* objs, unsigned count, uint64_t nunits, unsigned nlo,

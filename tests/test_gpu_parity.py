@@ -122,11 +122,13 @@ def test_decode_roundtrip_and_oracle(leo, k, r, b, loss):
 
 
 # The single-pass GF(2^16) decoder (k_dec16n_one: n <= 2048, <= 4 tiles of originals,
-# pieces >= 32 KiB): a tile mixing recovery and original positions (m = 128), a last
-# column strip of 8 units (B = 64 mod 128), lost recovery pieces, every original lost,
-# and callers' pointer tables (pieces scattered over the rows of a store).
-@pytest.mark.parametrize("k,r,b,loss,layout", [(300, 100, 33344, 60, "slab"), (1000, 200, 32832, 150, "scattered"),
-                                               (500, 500, 32768, 500, "slab")])
+# pieces >= 60 KiB): a tile mixing recovery and original positions (m = 128), a last
+# column strip of 8 units (B = 64 mod 128) in the 16-unit form and of one 64-byte
+# block in the 32-unit form (60-64 KiB pieces), lost recovery pieces, every
+# original lost, and callers' pointer tables (pieces scattered over a store's rows).
+@pytest.mark.parametrize("k,r,b,loss,layout", [(300, 100, 65600, 60, "slab"), (1000, 200, 61504, 150, "scattered"),
+                                               (500, 500, 65536, 500, "slab"), (1000, 200, 81984, 180, "slab"),
+                                               (600, 400, 65536, 300, "scattered")])
 def test_single_pass_ff16_decoder_matches_oracle(leo, k, r, b, loss, layout):
     rng = np.random.default_rng(k + r + loss)
     data = rng.integers(0, 256, (k, b), dtype=np.uint8)

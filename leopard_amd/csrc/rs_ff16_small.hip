@@ -907,7 +907,11 @@ constexpr int kDecOneR = LAMD_DEC16_ONE_R;
 // (profiles/r04_v21, r04_v22).  The host takes the one-pass form only from
 // 60 KiB pieces (fewer workgroups leave SIMDs idle: at 32 KiB it ran 96.7 us
 // against 87.2 for the two passes, at 48 KiB 145.8 against 139.7, at 56 KiB
-// 148.6 against 147.1; r04_v22, r04_v23).
+// 148.6 against 147.1; r04_v22, r04_v23).  With one workgroup per CU its LDS has
+// room for a second buffer of tables (each phase's skew set and scale / reveal
+// tables staged a whole phase ahead): measured 1-2% slower (152.4-153.4 vs
+// 150.9-152.5 us, r04_v24-v26) -- the boundary wait is the pieces', not the
+// tables', and the staging moved in front of the IFFT's first barrier.
 constexpr size_t kDecOneLds16 = one_lds_dwords<kDecOneR, 16>() * 4;
 constexpr size_t kDecOneLds32 = one_lds_dwords<kDecOneR, 32>() * 4;
 static_assert(kDecOneLds16 <= 160 * 1024 / 2 && kDecOneLds32 <= 160 * 1024, "two / one workgroup(s) per CU");

@@ -276,7 +276,7 @@ template <int T, int R, int LW>
 hipError_t launch_enc16n(const EncArgs& a, hipStream_t s) {
     using TL = Tile<FF16, T, R, 1, LW, 0, lg_bits(LW)>;
     constexpr size_t lds = (TL::kXchDwords + 2 * tab16_set_dwords(T)) * 4;
-    static_assert(lds <= 80 * 1024, "two workgroups per CU");
+    static_assert(lds <= (LW == 16 ? 80 : 160) * 1024, "two (16-unit strips) / one workgroup(s) per CU");
     static hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_enc16n<T, R, LW>),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
     if (attr != hipSuccess) return attr;
@@ -925,9 +925,19 @@ extern "C" __attribute__((visibility("default"))) int leo_amd_debug_stamps16(voi
 
 // m = 2^Tm with Tm = 7, 8 (m = 128, 256), narrow strips of 16 units.
 bool encode16_small_supported(unsigned Tm) { return Tm == 7 || Tm == 8; }
+// m = 128: 32-unit strips (8-wave workgroups instead of 4, the chunk tables
+// staged once per 256-byte strip) when that makes one full round of 240..256
+// workgroups, as the one-pass decoder: 200+100 x 64 KiB 19.45 vs 20.0 us.  For
+// m = 256 (16-wave workgroups, one per CU) it measured slower (53.5 vs 52.6 us
+// at 1000+200 x 64 KiB, profiles/r04_v27), so 16-unit strips stay there.
+#ifndef LAMD_ENC16N_LW32
+#define LAMD_ENC16N_LW32 1
+#endif
 hipError_t launch_encode16_small(unsigned Tm, const EncArgs& a, hipStream_t s) {
+    const uint64_t strips32 = (a.nunits + 31) / 32;
+    const bool wide = LAMD_ENC16N_LW32 && strips32 >= 240 && strips32 <= 256;
     switch (Tm) {
-        case 7: return launch_enc16n<7, 3, 16>(a, s);
+        case 7: return wide ? launch_enc16n<7, 3, 32>(a, s) : launch_enc16n<7, 3, 16>(a, s);
         case 8: return launch_enc16n<8, 3, 16>(a, s);
         default: return hipErrorInvalidValue;
     }

@@ -41,6 +41,8 @@ ENC_CASES = [
     # FF16 single-tile encoders (m <= 256) and multi-pass ones (m > 256)
     (129, 127, 64), (300, 37, 128), (1000, 200, 64), (700, 256, 128), (600, 300, 64), (5000, 3000, 64),
     (2000, 1000, 128),
+    # narrow-strip encoder on 32-unit strips (60-64 KiB pieces), m = 128 and 256, a last strip of 8 units
+    (200, 100, 65536), (1000, 200, 61504),
 ]
 
 

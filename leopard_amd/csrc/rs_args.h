@@ -196,6 +196,10 @@ hipError_t launch_ff8_encode_slab(unsigned T, const Ff8SlabBatch& b, unsigned co
                                   hipStream_t s);
 hipError_t launch_ff8_decode_batch(unsigned T, const Ff8DecArgs* objs, unsigned count, uint32_t nunits, int mode,
                                    hipStream_t s);
+// Bit-sliced dense tile (rs_ff8_bs.hip): slab batches of K = R = 128 codes,
+// form kFormDenseEnc or kFormDenseDec (the encoder's inverse, full loss).
+bool ff8_bs_supported(unsigned T, unsigned K, unsigned R, unsigned nchunks);
+hipError_t launch_ff8_bs_slab(const Ff8SlabBatch& b, unsigned count, int form, hipStream_t s);
 
 // Units per lane chosen for each kernel family (the host sizes grids with it).
 constexpr int kUnitsPerLane = 1;

@@ -771,6 +771,24 @@ bool force_wide() {
 #endif
 }
 
+// The bit-sliced dense tile (rs_ff8_bs.hip) for K = R = 128 slab batches; the
+// byte-layout tile stays selectable for A/B in experiment builds
+// (LEO_AMD_FF8_BS=0).
+#ifndef LAMD_FF8_BS
+#define LAMD_FF8_BS 1
+#endif
+bool bs_tile_enabled() {
+#if LAMD_EXPERIMENT_ENV
+    static const bool v = [] {
+        const char* e = std::getenv("LEO_AMD_FF8_BS");
+        return e ? e[0] == '1' : LAMD_FF8_BS != 0;
+    }();
+    return v;
+#else
+    return LAMD_FF8_BS != 0;
+#endif
+}
+
 // Lane-group bits of the encoder launch (LEO_AMD_FF8_G overrides; read once):
 // pieces of at most 64 KiB run 64-byte strips (G = 2: four workgroups per CU
 // in a 64 KiB call), larger pieces the full-wave strips.
@@ -946,6 +964,9 @@ hipError_t launch_ff8_encode_batch(unsigned T, const Ff8EncArgs* objs, unsigned 
 
 hipError_t launch_ff8_encode_slab(unsigned T, const Ff8SlabBatch& b, unsigned count, bool multi, int form,
                                   hipStream_t s) {
+    // dense 128 + 128 forms: the bit-sliced tile (rs_ff8_bs.hip)
+    if (form != kFormGeneral && !multi && bs_tile_enabled() && ff8_bs_supported(T, b.K, b.R, b.nchunks))
+        return launch_ff8_bs_slab(b, count, form, s);
     hipError_t e = hipErrorInvalidValue;
     static_for<1, 8>([&](auto I) {
         constexpr int TT = decltype(I)::value, RB = batch_bits8(TT);

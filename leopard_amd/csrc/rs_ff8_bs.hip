@@ -1,0 +1,443 @@
+// rs_ff8_bs.hip -- bit-sliced GF(2^8) dense tile for gfx950: batches of K = R = m = 128
+// codes (the benchmark's 128 + 128 shape), encode and full-loss decode.
+//
+// Reference path: ReedSolomonEncode (LeopardFF8.cpp:1602-1672) with one chunk,
+//   out = FFT_{-1}( IFFT_{m-1}(data) )            (IFFT_DIT / FFT_DIT, :595-666, :1319-1390)
+// and its inverse for a full-loss decode of such a code (rs_ff8.hip:
+// launch_ff8_decode_full), data = FFT_{m-1}( IFFT_{-1}(recovery) ).
+//
+// Why bit slices.  In the byte layout of rs_ff8.hip a multiply by a constant c
+// costs 3 v_perm_b32 + 5 selector ops + 2 XORs per 4 elements, and the tile is
+// bound by VALU issue.  Here a lane holds 32 elements of
+// a piece as 8 bit planes (plane k = bit k of 32 elements), so x ^= c * y is
+// the 8 x 8 GF(2) matrix of c applied to the planes: plane i of x takes the XOR
+// of the planes j of y that row i selects.  Every skew of the dense tile is
+// known at compile time (gf8_const.h), so most butterflies compile to a fixed
+// XOR network (~4x cheaper than the byte form, tools/ubench_bitslice8.hip).
+//
+// Tile: ONE wave owns the whole 128-piece transform over a 256-byte column
+// strip of every piece.  Lane = 8 * g + l: lane group g (8 groups), lane l of
+// the group holds bytes [16 l, 16 l + 16) and [128 + 16 l, 128 + 16 l + 16) of
+// the strip (32 elements = 8 dwords -> 8 planes) of 16 pieces:
+//   layout 0   (load, IFFT layers 0-2, FFT layers 2-0, store): register r holds
+//              piece r | g << 4 (piece bits 0-3 in registers, bits 4-6 = g);
+//   layout top (IFFT layers 3-5, fused top layer 6, FFT layers 5-3): register r
+//              holds piece g | r << 3 (bits 3-6 in registers, bits 0-2 = g).
+// A layer-l butterfly group's skew depends on the piece bits above l only
+// (skew index ((i >> l) | 1) << l).  In layout top those are register bits:
+// every multiplier is a compile-time constant.  In layout 0 the bits 4-6 come
+// from the lane group; the skews are affine in those bits (FFTInitialize builds
+// FFTSkew[first + k * 2^(l+1)] as the XOR of one generator per bit of k,
+// LeopardFF8.cpp:505-514; checked by static_assert below), so
+//   c(g) * y = A * y  ^  sum over bits b of g of  (g_b ? H_b * y : 0)
+// with A and H_b compile time and the selection by per-lane masks (v_bitop3).
+// The two layouts are exchanged through a wave-private LDS area (no barrier:
+// one wave's LDS operations execute in order).  No tables, no workgroup
+// barriers: waves are independent, several per SIMD.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "gf8_const.h"
+#include "rs_args.h"
+
+namespace lamd {
+
+namespace {
+
+#ifndef LAMD_BS_WAVES
+#define LAMD_BS_WAVES 4  // independent tiles (waves) per workgroup
+#endif
+constexpr int kBsWaves = LAMD_BS_WAVES;
+constexpr unsigned kBsBlocksPerCu = 8 / kBsWaves;  // workgroups per CU at LAMD_BS_OCC = 2
+constexpr unsigned kBsStrip = 256;           // bytes of every piece per wave
+constexpr unsigned kBsAreaDw = (128 + 8) * 8 * 2;  // LDS dwords per wave: 136 rows x 8 lanes x 2 planes
+#ifndef LAMD_BS_OCC
+#define LAMD_BS_OCC 2  // waves per SIMD the register budget is sized for
+#endif
+#ifndef LAMD_BS_SCHED
+#define LAMD_BS_SCHED 1  // 1: a scheduling barrier after every butterfly (bounds the temporaries in flight)
+#endif
+LDEV void bs_fence() {
+    if constexpr (LAMD_BS_SCHED) __builtin_amdgcn_sched_barrier(0);
+}
+
+// ---------------------------------------------------------- bit planes -----
+
+// v_bitop3_b32 truth tables: index = 4 * src0 + 2 * src1 + src2
+LDEV uint32_t sel_b(uint32_t a, uint32_t b, uint32_t m) { return __builtin_amdgcn_bitop3_b32(a, b, m, 0xD8); }  // m ? b : a
+LDEV uint32_t xor_and(uint32_t a, uint32_t b, uint32_t m) { return __builtin_amdgcn_bitop3_b32(a, b, m, 0x78); }  // a ^ (b & m)
+
+// Exchange the MASK << S bits of a (the low register) with the MASK bits of b.
+template <int S, uint32_t MASK>
+LDEV void mswap(uint32_t& a, uint32_t& b) {
+    const uint32_t na = sel_b(b << S, a, MASK);  // MASK ? a : b << S
+    const uint32_t nb = sel_b(b, a >> S, MASK);  // MASK ? a >> S : b
+    a = na;
+    b = nb;
+}
+// Exact 8 x 8 bit transpose in each byte lane of 8 dwords: afterwards plane k
+// bit (8 p + r) = bit k of byte p of dword r.  An involution (bytes <-> planes).
+LDEV void transpose8(uint32_t* v) {
+#ifdef ABL_XPOSE
+    return;
+#endif
+#pragma unroll
+    for (int i = 0; i < 4; ++i) mswap<4, 0x0F0F0F0Fu>(v[i], v[i + 4]);
+#pragma unroll
+    for (int i = 0; i < 8; i += 4)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) mswap<2, 0x33333333u>(v[i + j], v[i + j + 2]);
+#pragma unroll
+    for (int i = 0; i < 8; i += 2) mswap<1, 0x55555555u>(v[i], v[i + 1]);
+}
+
+LDEV uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
+// acc ^ (XOR of the planes y[j] with bit j of `row` set), as 3-input XORs
+template <unsigned row, int J = 0>
+LDEV uint32_t fold(uint32_t acc, const uint32_t* y) {
+    if constexpr (J >= 8 || (row >> J) == 0) {
+        return acc;
+    } else if constexpr (((row >> J) & 1u) == 0) {
+        return fold<row, J + 1>(acc, y);
+    } else {
+        constexpr unsigned rest = row & ~((2u << J) - 1u);  // bits above J
+        if constexpr (rest == 0) {
+            return acc ^ y[J];
+        } else {
+            constexpr int K = __builtin_ctz(rest);
+            return fold<row & ~((2u << K) - 1u), K + 1>(xor3(acc, y[J], y[K]), y);
+        }
+    }
+}
+// Keep a value materialised here: the networks are all XORs, and without a
+// fence the compiler reassociates them across butterflies and layers into
+// long-lived shared subexpressions (200+ VGPRs instead of the tile's 128).
+LDEV void pin8(uint32_t* v) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) asm volatile("" : "+v"(v[k]));
+}
+
+// x ^= M * y (M compile time: the multiply by a constant as an XOR network)
+template <uint64_t M>
+LDEV void mac(uint32_t* x, const uint32_t* y) {
+    static_for<0, 8>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        constexpr unsigned row = unsigned(M >> (8 * i)) & 0xFFu;
+        if constexpr (row != 0) x[i] = fold<row>(x[i], y);
+    });
+}
+// x ^= (M * y) & g  (g: a per-lane all-ones / all-zeros mask)
+template <uint64_t M>
+LDEV void mac_masked(uint32_t* x, const uint32_t* y, uint32_t g) {
+#ifdef ABL_MASKED
+    return;
+#endif
+    static_for<0, 8>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        constexpr unsigned row = unsigned(M >> (8 * i)) & 0xFFu;
+        if constexpr (row != 0) {
+            constexpr int J = __builtin_ctz(row);
+            x[i] = xor_and(x[i], fold<(row & ~(1u << J))>(y[J], y), g);
+        }
+    });
+}
+
+// ------------------------------------------------------------ skews --------
+
+constexpr unsigned sidx(unsigned p, unsigned l) { return ((p >> l) | 1u) << l; }
+constexpr unsigned skew_at(int off, unsigned p, unsigned l) { return gf8_skew(off + int(sidx(p, l))); }
+// lane-group part of a layout-0 skew: bit c of g = piece bit 4 + c
+constexpr unsigned twist(int off, unsigned r, unsigned l, unsigned c) {
+    return skew_at(off, r | (16u << c), l) ^ skew_at(off, r, l);
+}
+constexpr bool affine_ok() {
+    for (int off : {-1, 127})
+        for (unsigned l = 0; l < 3; ++l)
+            for (unsigned r = 0; r < 16; ++r)
+                for (unsigned g = 0; g < 8; ++g) {
+                    unsigned v = skew_at(off, r, l);
+                    for (unsigned c = 0; c < 3; ++c)
+                        if ((g >> c) & 1u) v ^= twist(off, r, l, c);
+                    if (v != skew_at(off, r | (g << 4), l)) return false;
+                }
+    return true;
+}
+static_assert(affine_ok(), "layout-0 skews are affine in the lane-group bits");
+
+// ----------------------------------------------------------- butterflies ---
+
+using Reg = uint32_t[16][8];
+
+// Layout 0, layer L in {0, 1, 2}: pairs (r, r + 2^L) of register bits 0-3.
+template <bool kInverse, int kOff, int L>
+LDEV void layer_low(Reg& x, const uint32_t (&G)[3]) {
+    constexpr int half = 1 << L;
+    static_for<0, 16>([&](auto RI) {
+        constexpr unsigned r = decltype(RI)::value;
+        if constexpr ((r & half) == 0) {
+            constexpr uint64_t A = gf8_matrix(skew_at(kOff, r, L));
+            constexpr uint64_t H0 = gf8_matrix(twist(kOff, r, L, 0));
+            constexpr uint64_t H1 = gf8_matrix(twist(kOff, r, L, 1));
+            constexpr uint64_t H2 = gf8_matrix(twist(kOff, r, L, 2));
+            uint32_t* a = x[r];
+            uint32_t* b = x[r + half];
+            if constexpr (kInverse) {  // IFFT_DIT2: y ^= x; x ^= y * skew
+#pragma unroll
+                for (int k = 0; k < 8; ++k) b[k] ^= a[k];
+            }
+            mac<A>(a, b);
+            mac_masked<H0>(a, b, G[0]);
+            mac_masked<H1>(a, b, G[1]);
+            mac_masked<H2>(a, b, G[2]);
+            if constexpr (!kInverse) {  // FFT_DIT2: x ^= y * skew; y ^= x
+#pragma unroll
+                for (int k = 0; k < 8; ++k) b[k] ^= a[k];
+            }
+            pin8(a);
+            pin8(b);
+            bs_fence();
+        }
+    });
+}
+// Layout top, layer L in {3, 4, 5}: pairs over register bit L - 3 (piece g | r << 3).
+template <bool kInverse, int kOff, int L>
+LDEV void layer_top(Reg& x) {
+    constexpr int half = 1 << (L - 3);
+    static_for<0, 16>([&](auto RI) {
+        constexpr unsigned r = decltype(RI)::value;
+        if constexpr ((r & half) == 0) {
+            constexpr uint64_t A = gf8_matrix(skew_at(kOff, r << 3, L));
+            uint32_t* a = x[r];
+            uint32_t* b = x[r + half];
+            if constexpr (kInverse) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) b[k] ^= a[k];
+            }
+            mac<A>(a, b);
+            if constexpr (!kInverse) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) b[k] ^= a[k];
+            }
+            pin8(a);
+            pin8(b);
+            bs_fence();
+        }
+    });
+}
+// The top IFFT layer (skew base kOffI) and the top FFT layer (kOffF) on the
+// same pairs (r, r + 8) as one butterfly with multiplier c1 + c2 (as
+// Tile::fused_top): y1 = y ^ x, x2 = x ^ (c1 + c2) y1, y2 = y1 ^ x2.
+template <int kOffI, int kOffF>
+LDEV void fused_top(Reg& x) {
+    constexpr uint64_t E = gf8_matrix(skew_at(kOffI, 64, 6) ^ skew_at(kOffF, 64, 6));
+    static_for<0, 8>([&](auto RI) {
+        constexpr unsigned r = decltype(RI)::value;
+        uint32_t* a = x[r];
+        uint32_t* b = x[r + 8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) b[k] ^= a[k];
+        mac<E>(a, b);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) b[k] ^= a[k];
+        pin8(a);
+        pin8(b);
+        bs_fence();
+    });
+}
+
+// --------------------------------------------------------- exchanges -------
+
+// LDS byte address of piece p, lane l in the wave's area: 64-byte rows of
+// 8 lanes x 8 bytes, one pad row after every 16 pieces,
+//   64 p + 64 (p >> 4) + 8 l,
+// so that the 8 lane groups of a layout-0 access (pieces 16 apart: 1088 g) and
+// of a layout-top access (pieces 1 apart: 64 g) fall in 4 different 64-byte
+// bank windows (two lanes per bank: the minimum for 8-byte accesses).  The
+// per-register part is a compile-time offset (the ds instruction's immediate).
+constexpr unsigned off0(unsigned r) { return 64u * r; }                               // layout 0, + lane part 1088 g + 8 l
+constexpr unsigned offT(unsigned r) { return 512u * r + 64u * (r >> 1); }            // layout top, + lane part 64 g + 8 l
+
+// Layout 0 -> top (kToTop) or back, in 4 rounds of 2 planes through the wave's area.
+template <bool kToTop>
+LDEV void exchange(Reg& x, uint8_t* area, unsigned g, unsigned l) {
+#ifdef ABL_XCH
+    return;
+#endif
+    Reg y;
+    uint8_t* const base0 = area + 1088u * g + 8u * l;
+    uint8_t* const baseT = area + 64u * g + 8u * l;
+    uint8_t* const wbase = kToTop ? base0 : baseT;
+    uint8_t* const rbase = kToTop ? baseT : base0;
+    static_for<0, 4>([&](auto Q) {
+        constexpr int q = decltype(Q)::value;
+        static_for<0, 16>([&](auto RI) {
+            constexpr unsigned r = decltype(RI)::value;
+            v2u v;
+            v.x = x[r][2 * q];
+            v.y = x[r][2 * q + 1];
+            *reinterpret_cast<v2u*>(wbase + (kToTop ? off0(r) : offT(r))) = v;
+        });
+        // one wave's LDS operations execute in order: the reads below see the
+        // writes above, and the next round's writes follow these reads
+        asm volatile("" ::: "memory");
+        static_for<0, 16>([&](auto RI) {
+            constexpr unsigned r = decltype(RI)::value;
+            const v2u v = *reinterpret_cast<const v2u*>(rbase + (kToTop ? offT(r) : off0(r)));
+            y[r][2 * q] = v.x;
+            y[r][2 * q + 1] = v.y;
+        });
+        asm volatile("" ::: "memory");
+    });
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) x[r][k] = y[r][k];
+}
+
+// -------------------------------------------------------------- kernel -----
+
+template <int kForm>
+LDEV void ff8_bs(const Ff8SlabView& a, uint8_t* area, unsigned strip) {
+    constexpr int kOffI = kForm == kFormDenseDec ? -1 : 127;  // IFFT skew base
+    constexpr int kOffF = kForm == kFormDenseDec ? 127 : -1;  // FFT skew base
+    const unsigned lane = threadIdx.x & 63u, g = lane >> 3, l = lane & 7u;
+    const uint32_t bytes = a.nunits * 4u;
+    const uint32_t rem = bytes - strip * kBsStrip;  // >= 64 (bytes % 64 == 0)
+    const uint32_t o0 = 16u * l, o1 = 128u + 16u * l;
+    const bool live0 = o0 + 16u <= rem, live1 = o1 + 16u <= rem;
+    const uint64_t col = uint64_t(strip) * kBsStrip;
+    const uint32_t G[3] = {(g & 1u) ? ~0u : 0u, (g & 2u) ? ~0u : 0u, (g & 4u) ? ~0u : 0u};
+
+    Reg x;
+    {
+        // pieces r | g << 4: a lane group reads 128 contiguous bytes per instruction
+        const uint8_t* base = reinterpret_cast<const uint8_t*>(a.in_base + col) + int64_t(g << 4) * a.in_stride;
+        const uint32_t l0 = live0 ? o0 : 0u, l1 = live1 ? o1 : 0u;  // past the end: re-read a valid segment
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+#ifdef ABL_LOAD
+            for (int k = 0; k < 8; ++k) x[r][k] = lane * (r + 3) + k * 77 + uint32_t(uintptr_t(base));
+            continue;
+#endif
+            const uint8_t* p = base + int64_t(r) * a.in_stride;
+#ifdef ABL_MEM
+            v4u v0, v1;
+            v0.x = uint32_t(uintptr_t(p)) + lane, v0.y = v0.x * 3, v0.z = v0.x * 5, v0.w = v0.x * 7;
+            v1 = v0 * 11u;
+#else
+            const v4u v0 = *gptr<const v4u>(p + l0);
+            const v4u v1 = *gptr<const v4u>(p + l1);
+#endif
+            x[r][0] = v0.x, x[r][1] = v0.y, x[r][2] = v0.z, x[r][3] = v0.w;
+            x[r][4] = v1.x, x[r][5] = v1.y, x[r][6] = v1.z, x[r][7] = v1.w;
+        }
+    }
+#ifndef ABL_ARITH
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        transpose8(x[r]);
+        pin8(x[r]);
+        bs_fence();
+    }
+
+    layer_low<true, kOffI, 0>(x, G);
+    layer_low<true, kOffI, 1>(x, G);
+    layer_low<true, kOffI, 2>(x, G);
+    exchange<true>(x, area, g, l);
+    layer_top<true, kOffI, 3>(x);
+    layer_top<true, kOffI, 4>(x);
+    layer_top<true, kOffI, 5>(x);
+    fused_top<kOffI, kOffF>(x);
+    layer_top<false, kOffF, 5>(x);
+    layer_top<false, kOffF, 4>(x);
+    layer_top<false, kOffF, 3>(x);
+    exchange<false>(x, area, g, l);
+    layer_low<false, kOffF, 2>(x, G);
+    layer_low<false, kOffF, 1>(x, G);
+    layer_low<false, kOffF, 0>(x, G);
+
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        transpose8(x[r]);
+        pin8(x[r]);
+        bs_fence();
+    }
+#endif
+    uint8_t* base = reinterpret_cast<uint8_t*>(a.out_base + col) + int64_t(g << 4) * a.out_stride;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        uint8_t* p = base + int64_t(r) * a.out_stride;
+        v4u v0, v1;
+        v0.x = x[r][0], v0.y = x[r][1], v0.z = x[r][2], v0.w = x[r][3];
+        v1.x = x[r][4], v1.y = x[r][5], v1.z = x[r][6], v1.w = x[r][7];
+#ifdef ABL_MEM
+        uint32_t acc = v0.x ^ v0.y ^ v0.z ^ v0.w ^ v1.x ^ v1.y ^ v1.z ^ v1.w;
+        if (acc == 0x12345679u && rem == 7u) *gptr<uint32_t>(p) = acc;  // keep the values live
+        continue;
+#endif
+        if (live0) *gptr<v4u>(p + o0) = v0;
+        if (live1) *gptr<v4u>(p + o1) = v1;
+    }
+}
+
+// Persistent waves: the grid fills the GPU once (kBsWaves waves a workgroup,
+// one workgroup a CU at two waves per SIMD) and wave i codes tiles i, i + n,
+// ... (tile = object * strips + strip).  Every tile is load -> ~10 us of
+// butterflies -> store; the two waves a SIMD holds start half a tile apart
+// (the waves kBsWaves / 2 .. kBsWaves - 1 of a workgroup, placed on the SIMDs
+// after the first half, sleep first), so that one computes while the other's
+// loads and stores are in flight, instead of both waiting on HBM at the same
+// time tile after tile.
+#ifndef LAMD_BS_STAGGER
+#define LAMD_BS_STAGGER 0  // s_sleep 127 (8128 cycles) steps of the second wave of a SIMD (measured: 1, 2, 4 slower)
+#endif
+template <int kForm>
+__global__ void __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(LAMD_BS_OCC, LAMD_BS_OCC)))
+k_ff8_bs_slab(Ff8SlabBatch b, uint32_t count, uint32_t strips) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const unsigned wave = threadIdx.x >> 6;
+    const unsigned n = gridDim.x * kBsWaves, total = count * strips;
+    uint8_t* const area = reinterpret_cast<uint8_t*>(lds + wave * kBsAreaDw);
+    unsigned t = blockIdx.x * kBsWaves + wave;
+    if (wave >= kBsWaves / 2 && t + n < total)
+        for (int i = 0; i < LAMD_BS_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
+    for (; t < total; t += n) {
+        const unsigned obj = t / strips, strip = t - obj * strips;
+        ff8_bs<kForm>(Ff8SlabView(b, obj), area, strip);
+    }
+}
+
+}  // namespace
+
+bool ff8_bs_supported(unsigned T, unsigned K, unsigned R, unsigned nchunks) {
+    return T == 7 && K == 128 && R == 128 && nchunks == 1;
+}
+
+hipError_t launch_ff8_bs_slab(const Ff8SlabBatch& b, unsigned count, int form, hipStream_t s) {
+    if (count == 0 || count > kSlabObjs || (b.nunits * 4u) % 64u != 0 || b.K != 128 || b.R != 128)
+        return hipErrorInvalidValue;
+    if (form != kFormDenseEnc && form != kFormDenseDec) return hipErrorInvalidValue;
+    static int cus[64] = {};  // compute units per device (queried once)
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    if (cus[dev] == 0) {
+        int n = 0;
+        e = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+        if (e != hipSuccess) return e;
+        cus[dev] = n > 0 ? n : 1;
+    }
+    uint32_t strips = (b.nunits * 4u + kBsStrip - 1) / kBsStrip;
+    uint32_t cnt = count;
+    const unsigned total = cnt * strips;
+    const unsigned blocks = std::min<unsigned>((total + kBsWaves - 1) / kBsWaves, unsigned(cus[dev]) * kBsBlocksPerCu);
+    const size_t lds = size_t(kBsWaves) * kBsAreaDw * 4;
+    void* params[] = {const_cast<Ff8SlabBatch*>(&b), &cnt, &strips};
+    const void* fn = form == kFormDenseDec ? reinterpret_cast<const void*>(&k_ff8_bs_slab<kFormDenseDec>)
+                                           : reinterpret_cast<const void*>(&k_ff8_bs_slab<kFormDenseEnc>);
+    return hipLaunchKernel(fn, dim3(blocks), dim3(64 * kBsWaves), params, lds, s);
+}
+
+}  // namespace lamd

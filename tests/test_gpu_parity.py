@@ -641,6 +641,34 @@ def test_batch_encode_decode_match_oracle(leo, k, r, b, layout):
             assert np.array_equal(got[i], objs[o][i]), (o, i)
 
 
+@pytest.mark.parametrize("b", [64, 192, 256, 64 * 37, 65536 + 192])
+def test_bitsliced_dense_tile_matches_oracle(leo, b):
+    """The bit-sliced tile (rs_ff8_bs.hip) that runs slab batches of 128 + 128
+    codes: encode against the oracle, full-loss decode back to the originals,
+    on piece sizes that end in a partial 256-byte strip (64 / 128 / 192 bytes
+    left) and in several launches' worth of objects (70 > 64 per launch)."""
+    k = r = 128
+    count = 3 if b > 4096 else 70
+    objs = _batch_objects(k, r, b, count, b)
+    dev = [dev_tensor(d) for d in objs]
+    wc, dwc = leo.leo_encode_work_count(k, r), leo.leo_decode_work_count(k, r)
+    works = [torch.zeros((wc, b), dtype=torch.uint8, device="cuda") for _ in range(count)]
+    res = leo.leo_amd_encode_batch(b, k, r, wc, [[t[i].data_ptr() for i in range(k)] for t in dev],
+                                   [[w[i].data_ptr() for i in range(wc)] for w in works])
+    assert res == leo.LeopardResult.Success, leo.last_error()
+    torch.cuda.synchronize()
+    for o in ([0, 1, count - 1] if count > 3 else range(count)):
+        assert np.array_equal(works[o][:r].cpu().numpy(), ol.oracle().encode(objs[o], r)), o
+    dworks = [torch.zeros((dwc, b), dtype=torch.uint8, device="cuda") for _ in range(count)]
+    res = leo.leo_amd_decode_batch(b, k, r, dwc, [[None] * k] * count,
+                                   [[w[i].data_ptr() for i in range(r)] for w in works],
+                                   [[w[i].data_ptr() for i in range(dwc)] for w in dworks])
+    assert res == leo.LeopardResult.Success, leo.last_error()
+    torch.cuda.synchronize()
+    for o in range(count):
+        assert torch.equal(dworks[o][:k], dev[o]), o
+
+
 def test_batch_full_loss_and_validation(leo):
     """The benchmark's batch (every original lost, the half-position decoder in
     one launch) and the batch validation rules."""

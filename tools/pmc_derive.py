@@ -23,7 +23,9 @@ def main():
         print(f"{k[:58]:58s} cyc={cyc / 1e3:8.1f}K valu_busy={busy:4.2f} valu/wave={v['SQ_INSTS_VALU'] / v['SQ_WAVES']:7.0f} "
               f"lds/wave={v['SQ_INSTS_LDS'] / v['SQ_WAVES']:5.0f} salu/wave={v['SQ_INSTS_SALU'] / v['SQ_WAVES']:5.0f} "
               f"wait_any={v['SQ_WAIT_ANY'] / wc:4.2f} wait_inst={v['SQ_WAIT_INST_ANY'] / wc:4.2f} "
-              f"active={v['SQ_ACTIVE_INST_ANY'] / wc:4.2f} hbm={(v.get('FETCH_SIZE', 0) * 2 + v.get('WRITE_SIZE', 0)) / 1e3:7.2f}MB")
+              f"active={v['SQ_ACTIVE_INST_ANY'] / wc:4.2f} hbm={(v.get('FETCH_SIZE', 0) * 2 + v.get('WRITE_SIZE', 0)) / 1e3:7.2f}MB"
+              + (f" icache_miss={v['SQC_ICACHE_MISSES'] / max(v.get('SQC_ICACHE_REQ', 1), 1):5.3f}"
+                 f" icache_req/wave={v.get('SQC_ICACHE_REQ', 0) / v['SQ_WAVES']:7.0f}" if "SQC_ICACHE_MISSES" in v else ""))
 
 
 if __name__ == "__main__":

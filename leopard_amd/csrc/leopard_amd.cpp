@@ -94,6 +94,9 @@ struct DeviceTables {
     bool ready = false;
 };
 
+// Bytes of freed stream-ordered memory the library's pool keeps per device.
+constexpr uint64_t kPoolKeepBytes = 256ull << 20;
+
 std::mutex g_mu;
 bool g_initialized = false;
 int g_device_count = 0;
@@ -136,8 +139,13 @@ LeopardResult ensure_device(int dev, DeviceTables** out) {
         props.location.type = hipMemLocationTypeDevice;
         props.location.id = dev;
         HIP_OK(hipMemPoolCreate(&d.pool, &props), "workspace memory pool");
-        // keep freed blocks for reuse until release_device_memory trims the pool
-        uint64_t keep = UINT64_MAX;
+        // Freed blocks up to kPoolKeepBytes stay in the pool for reuse (a call's
+        // scratch, the ring, small direct rows); above that the pool returns
+        // memory to the device at the next synchronisation, so one-off large
+        // allocations (direct rows of a big host call, an arena replaced by a
+        // larger one) are not held idle against the application's own
+        // allocations.  release_device_memory trims the rest.
+        uint64_t keep = kPoolKeepBytes;
         HIP_OK(hipMemPoolSetAttribute(d.pool, hipMemPoolAttrReleaseThreshold, &keep), "pool release threshold");
         d.ready = true;
     }
@@ -1180,9 +1188,10 @@ LeopardResult decode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
     // (rs_ff16_small.hip), whose only intermediate is U (tiles with received data).
     const unsigned ntiles_in = (m + K + (1u << kLoBits) - 1) >> kLoBits;
     const bool narrow = g_q16_ok && decode16_small_supported(Tn) && bytes <= kNarrowColumnsMax;
-    // few output tiles and enough column strips to fill the GPU (>= 32 KiB
-    // pieces: 256 strips): the one-pass form (no U slab); narrower calls keep
-    // the two passes, whose grids also spread over the tiles
+    // few output tiles and pieces of at least kOnePassMinBytes (60 KiB: below
+    // that the one-pass grid leaves SIMDs idle and measured slower, 32 KiB
+    // 96.7 vs 87.2 us, rs_ff16_small.hip): the one-pass form (no U slab);
+    // narrower calls keep the two passes, whose grids also spread over the tiles
     const bool one_pass = narrow && bytes >= kOnePassMinBytes &&
                           decode16_one_supported(((m + K - 1) >> kLoBits) - (m >> kLoBits) + 1);
     const uint64_t slab_pieces = one_pass ? 0 : narrow ? uint64_t(ntiles_in) << kLoBits : 2ull * n;  // U (+ A, multi-pass)
@@ -2163,7 +2172,11 @@ LeopardResult encode_batch16(int dev, unsigned count, uint64_t bytes, unsigned K
 }
 
 // Decoder: objects in chunks of kDec16Slots (each object's erasure pattern
-// holds a decoder-state slot for the chunk), a U slab per object.
+// holds a decoder-state slot for the chunk), a U slab per object, at most
+// kBatch16SlabBytes of slabs a chunk.  Only for pieces under kOnePassMinBytes:
+// larger pieces decode object by object in the one-pass form (no slab), whose
+// single-object grid already fills the GPU.
+constexpr uint64_t kBatch16SlabBytes = 256ull << 20;
 LeopardResult decode_batch16(int dev, unsigned count, uint64_t bytes, unsigned K, unsigned R,
                              const void* const* const* orig, const void* const* const* rec, void** const* work) {
     DeviceGuard guard(dev);
@@ -2175,8 +2188,10 @@ LeopardResult decode_batch16(int dev, unsigned count, uint64_t bytes, unsigned K
     const unsigned ntiles_in = (m + K + (1u << kLoBits) - 1) >> kLoBits;
     const unsigned tile0 = m >> kLoBits, nout = ((m + K - 1) >> kLoBits) - tile0 + 1;
     const uint64_t slab = (uint64_t(ntiles_in) << kLoBits) * bytes;  // U of one object
-    for (unsigned o0 = 0; o0 < count; o0 += Workspace::kDec16Slots) {
-        const unsigned nb = std::min(Workspace::kDec16Slots, count - o0);
+    const unsigned per_chunk = unsigned(std::max<uint64_t>(1, std::min<uint64_t>(Workspace::kDec16Slots,
+                                                                                  kBatch16SlabBytes / slab)));
+    for (unsigned o0 = 0; o0 < count; o0 += per_chunk) {
+        const unsigned nb = std::min(per_chunk, count - o0);
         ++ws.dec16_call;
         std::vector<DecArgs> args(nb);
         MapBuilder mb;
@@ -2357,7 +2372,7 @@ LeopardResult decode_batch(unsigned count, uint64_t bytes, unsigned K, unsigned 
                 for (unsigned i = 0; i < K && on_dev; ++i)
                     if (!orig[o][i]) on_dev = rc.on(work[o][i], bytes, d16);
             }
-            if (on_dev) return decode_batch16(d16, count, bytes, K, R, orig, rec, work);
+            if (on_dev && bytes < kOnePassMinBytes) return decode_batch16(d16, count, bytes, K, R, orig, rec, work);
         }
     }
     for (unsigned o = 0; o < count; ++o) {

@@ -789,15 +789,18 @@ bool bs_tile_enabled() {
 #endif
 }
 
-// Lane-group bits of the encoder launch (LEO_AMD_FF8_G overrides; read once):
+// Lane-group bits of the encoder launch (LEO_AMD_FF8_G overrides in experiment
+// builds, LAMD_EXPERIMENT_ENV=1: lib/exp/libleopard_amd.so; read once):
 // pieces of at most 64 KiB run 64-byte strips (G = 2: four workgroups per CU
 // in a 64 KiB call), larger pieces the full-wave strips.
 int enc_lane_groups(uint32_t nunits) {
+#if LAMD_EXPERIMENT_ENV
     static const int v = [] {
         const char* e = std::getenv("LEO_AMD_FF8_G");
         return e && e[0] >= '0' && e[0] <= '2' ? e[0] - '0' : -1;
     }();
     if (v >= 0) return v;
+#endif
     return nunits <= 16384u ? kDefaultEncG : 0;
 }
 

@@ -153,6 +153,30 @@ def test_scratch_bounded_over_fresh_streams(leo):
     assert _settled(base) <= 8 * MiB, "device memory not returned by leo_amd_release_stream"
 
 
+def test_large_host_call_returns_its_device_rows(leo):
+    """A pageable host call whose direct-copy rows exceed the kept budget
+    (128 + 128 pieces of 2 MiB: 512 MiB of device rows) frees them after the
+    call, and the library's memory pool hands them back to the device (its
+    release threshold is finite, 256 MiB): device memory in use afterwards
+    stays within that budget of where it started.  The recovery data equals a
+    device-resident encode of the same pieces."""
+    k = r = 128
+    b = 2 * MiB
+    data = np.random.default_rng(11).integers(0, 256, (k, b), dtype=np.uint8)
+    work = np.zeros((leo.leo_encode_work_count(k, r), b), dtype=np.uint8)
+    d_data = torch.from_numpy(data).cuda()
+    d_work = torch.zeros(work.shape, dtype=torch.uint8, device="cuda")
+    assert leo.leo_encode(b, k, r, work.shape[0], [d_data[i].data_ptr() for i in range(k)],
+                          [d_work[i].data_ptr() for i in range(work.shape[0])]) == leo.LeopardResult.Success
+    base = _free_mem()
+    assert leo.leo_encode(b, k, r, work.shape[0], [data[i].ctypes.data for i in range(k)],
+                          [work[i].ctypes.data for i in range(work.shape[0])]) == leo.LeopardResult.Success, \
+        leo.last_error()
+    used = _settled(base, tol=300 * MiB)
+    assert used <= 300 * MiB, f"{used / MiB:.0f} MiB of device memory still held after a 512 MiB host call"
+    assert np.array_equal(work[:r], d_work[:r].cpu().numpy())
+
+
 def test_async_calls_then_release_wait_for_the_work(leo):
     """Release right after async calls: the scratch is freed only after the
     queued kernels that read it are done (results stay correct)."""

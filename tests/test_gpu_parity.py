@@ -41,8 +41,9 @@ ENC_CASES = [
     # FF16 single-tile encoders (m <= 256) and multi-pass ones (m > 256)
     (129, 127, 64), (300, 37, 128), (1000, 200, 64), (700, 256, 128), (600, 300, 64), (5000, 3000, 64),
     (2000, 1000, 128),
-    # narrow-strip encoder on 32-unit strips (60-64 KiB pieces), m = 128 and 256, a last strip of 8 units
-    (200, 100, 65536), (1000, 200, 61504),
+    # narrow-strip encoder: m = 128 on 32-unit strips (60-64 KiB pieces), full strips and a
+    # last strip of 8 units (61504 B = 240 strips of 32 units + 8); m = 256 on 16-unit strips
+    (200, 100, 65536), (300, 100, 61504), (1000, 200, 61504),
 ]
 
 
@@ -510,10 +511,14 @@ def test_host_edge_paths(leo):
 @pytest.mark.gpu
 @pytest.mark.parametrize("groups", [1, 2])
 def test_encoder_lane_group_forms(groups):
-    """The lane-group encoder forms (LEO_AMD_FF8_G, read once per process) vs the oracle."""
+    """The lane-group encoder forms vs the oracle.  They are A/B forms, not the
+    product's: LEO_AMD_FF8_G (read once per process) selects them only in the
+    experiment build of the library (lib/exp, LAMD_EXPERIMENT_ENV=1)."""
     import subprocess
     import sys
-    env = dict(os.environ, LEO_AMD_FF8_G=str(groups))
+    exp = os.path.join(os.path.dirname(GOLDEN), "..", "leopard_amd", "lib", "exp", "libleopard_amd.so")
+    assert os.path.exists(exp), "make -C leopard_amd builds the experiment library"
+    env = dict(os.environ, LEO_AMD_FF8_G=str(groups), LEOPARD_AMD_LIB=os.path.abspath(exp))
     tool = os.path.join(os.path.dirname(GOLDEN), "..", "tools", "probe_g.py")
     res = subprocess.run([sys.executable, tool], env=env, capture_output=True, text=True, timeout=110)
     assert res.returncode == 0, res.stdout + res.stderr
@@ -667,6 +672,50 @@ def test_bitsliced_dense_tile_matches_oracle(leo, b):
     torch.cuda.synchronize()
     for o in range(count):
         assert torch.equal(dworks[o][:k], dev[o]), o
+
+
+def test_decoder_pattern_caches_evict_and_refill(leo):
+    """The per-workspace erasure-pattern caches under eviction: 600 distinct
+    GF(2^8) patterns (more than the 512 error-locator slots) and 20 GF(2^16)
+    patterns (more than the 16 decoder-state slots) on one stream, then the
+    earliest patterns again -- as single calls (for GF(2^8) the locator then
+    travels by value) and as one batch.  Every decode must rebuild the lost
+    originals; a stale slot would decode with another pattern's locator."""
+    torch.cuda.synchronize()
+    for k, r, b, npat, nbatch in [(100, 20, 64, 600, 16), (300, 100, 128, 20, 4)]:
+        rng = np.random.default_rng(k + npat)
+        data = rng.integers(0, 256, (k, b), dtype=np.uint8)
+        rec = ol.oracle().encode(data, r)
+        d_data, d_rec = dev_tensor(data), dev_tensor(rec)
+        dwc = leo.leo_decode_work_count(k, r)
+        pats, seen = [], set()
+        while len(pats) < npat:
+            loss = int(rng.integers(1, r + 1))
+            lo = tuple(sorted(rng.choice(k, loss, replace=False).tolist()))
+            lr = tuple(sorted(rng.choice(r, r - loss, replace=False).tolist()))
+            if (lo, lr) not in seen:
+                seen.add((lo, lr))
+                pats.append((set(lo), set(lr)))
+        order = list(range(npat)) + list(range(min(12, npat)))  # then the earliest (evicted) patterns again
+        works = [torch.zeros((dwc, b), dtype=torch.uint8, device="cuda") for _ in order]
+
+        def args(j, w):
+            lo, lr = pats[j]
+            return ([None if i in lo else d_data[i].data_ptr() for i in range(k)],
+                    [None if i in lr else d_rec[i].data_ptr() for i in range(r)], [w[i].data_ptr() for i in range(dwc)])
+
+        for j, w in zip(order, works):
+            res = leo.leo_decode(b, k, r, dwc, *args(j, w))
+            assert res == leo.LeopardResult.Success, leo.last_error()
+        bworks = [torch.zeros((dwc, b), dtype=torch.uint8, device="cuda") for _ in range(nbatch)]
+        ba = [args(j, w) for j, w in zip(range(nbatch), bworks)]
+        res = leo.leo_amd_decode_batch(b, k, r, dwc, [a[0] for a in ba], [a[1] for a in ba], [a[2] for a in ba])
+        assert res == leo.LeopardResult.Success, leo.last_error()
+        torch.cuda.synchronize()
+        for j, w in list(zip(order, works)) + list(zip(range(nbatch), bworks)):
+            got = w.cpu().numpy()
+            for i in pats[j][0]:
+                assert np.array_equal(got[i], data[i]), (k, r, j, i)
 
 
 def test_batch_full_loss_and_validation(leo):

@@ -68,28 +68,56 @@ LDEV void bs_fence() {
 LDEV uint32_t sel_b(uint32_t a, uint32_t b, uint32_t m) { return __builtin_amdgcn_bitop3_b32(a, b, m, 0xD8); }  // m ? b : a
 LDEV uint32_t xor_and(uint32_t a, uint32_t b, uint32_t m) { return __builtin_amdgcn_bitop3_b32(a, b, m, 0x78); }  // a ^ (b & m)
 
-// Exchange the MASK << S bits of a (the low register) with the MASK bits of b.
-template <int S, uint32_t MASK>
-LDEV void mswap(uint32_t& a, uint32_t& b) {
-    const uint32_t na = sel_b(b << S, a, MASK);  // MASK ? a : b << S
-    const uint32_t nb = sel_b(b, a >> S, MASK);  // MASK ? a >> S : b
-    a = na;
-    b = nb;
+// The transpose's three bit masks in VGPRs: v_bitop3_b32 with an SGPR (or
+// literal) operand issues at ~4.2 cycles a wave64 instruction against ~2.5
+// with three VGPRs (tools/ubench_issue.hip).
+struct XMasks {
+    uint32_t m4, m2, m1;
+    LDEV XMasks() : m4(0x0F0F0F0Fu), m2(0x33333333u), m1(0x55555555u) {
+        asm volatile("" : "+v"(m4), "+v"(m2), "+v"(m1));
+    }
+};
+// Delta-swap stage S on register pairs (lo[i], hi[i]), i = 0, 1, 2, 3: the
+// MASK << S bits of lo[i] are exchanged with the MASK bits of hi[i]:
+//   lo' = MASK ? lo : hi << S,   hi' = MASK ? lo >> S : hi.
+// The shifts run as 64-bit shifts of register pairs (hi[0], hi[1]) and
+// (lo[0], lo[1]) (a shift costs ~4 cycles a wave64 instruction whatever its
+// width): the bits one dword's shift carries into its neighbour land only where
+// the select takes the other operand (MASK has its top S bits clear and MASK << S
+// its low S bits).
+template <int S>
+LDEV void dstage(uint32_t* const (&lo)[4], uint32_t* const (&hi)[4], uint32_t mask) {
+    uint32_t hs[4], ls[4];
+#pragma unroll
+    for (int i = 0; i < 4; i += 2) {
+        // raw 64-bit shifts (the compiler would keep the carried bits exact
+        // with v_alignbit / v_or pairs)
+        v2u h0, l0, h, l;
+        h0.x = *hi[i], h0.y = *hi[i + 1];
+        l0.x = *lo[i], l0.y = *lo[i + 1];
+        asm("v_lshlrev_b64 %0, %1, %2" : "=v"(h) : "i"(S), "v"(h0));
+        asm("v_lshrrev_b64 %0, %1, %2" : "=v"(l) : "i"(S), "v"(l0));
+        hs[i] = h.x, hs[i + 1] = h.y;
+        ls[i] = l.x, ls[i + 1] = l.y;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t a = *lo[i], b = *hi[i];
+        *lo[i] = sel_b(hs[i], a, mask);
+        *hi[i] = sel_b(b, ls[i], mask);
+    }
 }
 // Exact 8 x 8 bit transpose in each byte lane of 8 dwords: afterwards plane k
 // bit (8 p + r) = bit k of byte p of dword r.  An involution (bytes <-> planes).
-LDEV void transpose8(uint32_t* v) {
+// The three stages commute (each exchanges one register-index bit with one
+// bit-in-byte index bit).
+LDEV void transpose8(uint32_t* v, const XMasks& m) {
 #ifdef ABL_XPOSE
     return;
 #endif
-#pragma unroll
-    for (int i = 0; i < 4; ++i) mswap<4, 0x0F0F0F0Fu>(v[i], v[i + 4]);
-#pragma unroll
-    for (int i = 0; i < 8; i += 4)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) mswap<2, 0x33333333u>(v[i + j], v[i + j + 2]);
-#pragma unroll
-    for (int i = 0; i < 8; i += 2) mswap<1, 0x55555555u>(v[i], v[i + 1]);
+    dstage<4>({&v[0], &v[1], &v[2], &v[3]}, {&v[4], &v[5], &v[6], &v[7]}, m.m4);
+    dstage<2>({&v[0], &v[1], &v[4], &v[5]}, {&v[2], &v[3], &v[6], &v[7]}, m.m2);
+    dstage<1>({&v[0], &v[4], &v[2], &v[6]}, {&v[1], &v[5], &v[3], &v[7]}, m.m1);
 }
 
 LDEV uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
@@ -308,6 +336,7 @@ LDEV void ff8_bs(const Ff8SlabView& a, uint8_t* area, unsigned strip) {
     const bool live0 = o0 + 16u <= rem, live1 = o1 + 16u <= rem;
     const uint64_t col = uint64_t(strip) * kBsStrip;
     const uint32_t G[3] = {(g & 1u) ? ~0u : 0u, (g & 2u) ? ~0u : 0u, (g & 4u) ? ~0u : 0u};
+    const XMasks xm;
 
     Reg x;
     {
@@ -336,7 +365,7 @@ LDEV void ff8_bs(const Ff8SlabView& a, uint8_t* area, unsigned strip) {
 #ifndef ABL_ARITH
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-        transpose8(x[r]);
+        transpose8(x[r], xm);
         pin8(x[r]);
         bs_fence();
     }
@@ -359,7 +388,7 @@ LDEV void ff8_bs(const Ff8SlabView& a, uint8_t* area, unsigned strip) {
 
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-        transpose8(x[r]);
+        transpose8(x[r], xm);
         pin8(x[r]);
         bs_fence();
     }

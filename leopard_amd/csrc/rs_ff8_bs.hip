@@ -48,13 +48,13 @@ namespace {
 #ifndef LAMD_BS_WAVES
 #define LAMD_BS_WAVES 4  // independent tiles (waves) per workgroup
 #endif
-constexpr int kBsWaves = LAMD_BS_WAVES;
-constexpr unsigned kBsBlocksPerCu = 8 / kBsWaves;  // workgroups per CU at LAMD_BS_OCC = 2
-constexpr unsigned kBsStrip = 256;           // bytes of every piece per wave
-constexpr unsigned kBsAreaDw = (128 + 8) * 8 * 2;  // LDS dwords per wave: 136 rows x 8 lanes x 2 planes
 #ifndef LAMD_BS_OCC
 #define LAMD_BS_OCC 2  // waves per SIMD the register budget is sized for
 #endif
+constexpr int kBsWaves = LAMD_BS_WAVES;
+constexpr unsigned kBsBlocksPerCu = 4 * LAMD_BS_OCC / kBsWaves;  // workgroups per CU (LAMD_BS_OCC waves per SIMD)
+constexpr unsigned kBsStrip = 256;           // bytes of every piece per wave
+constexpr unsigned kBsAreaDw = (128 + 8) * 8 * 2;  // LDS dwords per wave: 136 rows x 8 lanes x 2 planes
 #ifndef LAMD_BS_SCHED
 #define LAMD_BS_SCHED 1  // 1: a scheduling barrier after every butterfly (bounds the temporaries in flight)
 #endif
@@ -197,11 +197,12 @@ static_assert(affine_ok(), "layout-0 skews are affine in the lane-group bits");
 
 using Reg = uint32_t[16][8];
 
-// Layout 0, layer L in {0, 1, 2}: pairs (r, r + 2^L) of register bits 0-3.
-template <bool kInverse, int kOff, int L>
+// Layout 0, layer L in {0, 1, 2}: pairs (r, r + 2^L) of register bits 0-3, in
+// the half r = R0 .. R0 + 7 (the pairs never cross halves).
+template <bool kInverse, int kOff, int L, int R0>
 LDEV void layer_low(Reg& x, const uint32_t (&G)[3]) {
     constexpr int half = 1 << L;
-    static_for<0, 16>([&](auto RI) {
+    static_for<R0, R0 + 8>([&](auto RI) {
         constexpr unsigned r = decltype(RI)::value;
         if constexpr ((r & half) == 0) {
             constexpr uint64_t A = gf8_matrix(skew_at(kOff, r, L));
@@ -325,115 +326,150 @@ LDEV void exchange(Reg& x, uint8_t* area, unsigned g, unsigned l) {
 
 // -------------------------------------------------------------- kernel -----
 
-template <int kForm>
-LDEV void ff8_bs(const Ff8SlabView& a, uint8_t* area, unsigned strip) {
-    constexpr int kOffI = kForm == kFormDenseDec ? -1 : 127;  // IFFT skew base
-    constexpr int kOffF = kForm == kFormDenseDec ? 127 : -1;  // FFT skew base
-    const unsigned lane = threadIdx.x & 63u, g = lane >> 3, l = lane & 7u;
-    const uint32_t bytes = a.nunits * 4u;
-    const uint32_t rem = bytes - strip * kBsStrip;  // >= 64 (bytes % 64 == 0)
+// Where one tile (object, 256-byte column strip) lives for this lane.
+struct BsTile {
+    const uint8_t* in;   // piece g << 4 of the strip, + lane offset
+    uint8_t* out;
+    int32_t in_stride, out_stride;
+    uint32_t l0, l1;     // offsets of the lane's two 16-byte segments (past the piece's end: segment 0)
+};
+LDEV BsTile bs_tile(const Ff8SlabBatch& b, unsigned t, unsigned strips, unsigned g, unsigned l) {
+    const unsigned obj = t / strips, strip = t - obj * strips;
+    const uint32_t rem = b.nunits * 4u - strip * kBsStrip;  // >= 64 (bytes % 64 == 0)
     const uint32_t o0 = 16u * l, o1 = 128u + 16u * l;
-    const bool live0 = o0 + 16u <= rem, live1 = o1 + 16u <= rem;
+    BsTile T;
+    T.in_stride = b.in_stride[obj];
+    T.out_stride = b.out_stride[obj];
     const uint64_t col = uint64_t(strip) * kBsStrip;
-    const uint32_t G[3] = {(g & 1u) ? ~0u : 0u, (g & 2u) ? ~0u : 0u, (g & 4u) ? ~0u : 0u};
-    const XMasks xm;
-
-    Reg x;
-    {
-        // pieces r | g << 4: a lane group reads 128 contiguous bytes per instruction
-        const uint8_t* base = reinterpret_cast<const uint8_t*>(a.in_base + col) + int64_t(g << 4) * a.in_stride;
-        const uint32_t l0 = live0 ? o0 : 0u, l1 = live1 ? o1 : 0u;  // past the end: re-read a valid segment
+    T.in = reinterpret_cast<const uint8_t*>(b.in_base[obj] + col) + int64_t(g << 4) * T.in_stride;
+    T.out = reinterpret_cast<uint8_t*>(b.out_base[obj] + col) + int64_t(g << 4) * T.out_stride;
+    T.l0 = o0 + 16u <= rem ? o0 : 0u;
+    T.l1 = o1 + 16u <= rem ? o1 : 0u;
+    return T;
+}
+// Pieces r0 .. r0 + 7 (| g << 4) of a tile: a lane group reads 128 contiguous
+// bytes per instruction.
+template <int R0>
+LDEV void load_half(Reg& x, const BsTile& T) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-#ifdef ABL_LOAD
-            for (int k = 0; k < 8; ++k) x[r][k] = lane * (r + 3) + k * 77 + uint32_t(uintptr_t(base));
-            continue;
-#endif
-            const uint8_t* p = base + int64_t(r) * a.in_stride;
+    for (int r = R0; r < R0 + 8; ++r) {
+        const uint8_t* p = T.in + int64_t(r) * T.in_stride;
 #ifdef ABL_MEM
-            v4u v0, v1;
-            v0.x = uint32_t(uintptr_t(p)) + lane, v0.y = v0.x * 3, v0.z = v0.x * 5, v0.w = v0.x * 7;
-            v1 = v0 * 11u;
+        v4u v0, v1;
+        v0.x = uint32_t(uintptr_t(p)) + threadIdx.x, v0.y = v0.x * 3, v0.z = v0.x * 5, v0.w = v0.x * 7;
+        v1 = v0 * 11u;
 #else
-            const v4u v0 = *gptr<const v4u>(p + l0);
-            const v4u v1 = *gptr<const v4u>(p + l1);
+        const v4u v0 = *gptr<const v4u>(p + T.l0);
+        const v4u v1 = *gptr<const v4u>(p + T.l1);
 #endif
-            x[r][0] = v0.x, x[r][1] = v0.y, x[r][2] = v0.z, x[r][3] = v0.w;
-            x[r][4] = v1.x, x[r][5] = v1.y, x[r][6] = v1.z, x[r][7] = v1.w;
-        }
+        x[r][0] = v0.x, x[r][1] = v0.y, x[r][2] = v0.z, x[r][3] = v0.w;
+        x[r][4] = v1.x, x[r][5] = v1.y, x[r][6] = v1.z, x[r][7] = v1.w;
     }
-#ifndef ABL_ARITH
+}
+template <int R0>
+LDEV void store_half(const Reg& x, const BsTile& T) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        transpose8(x[r], xm);
-        pin8(x[r]);
-        bs_fence();
-    }
-
-    layer_low<true, kOffI, 0>(x, G);
-    layer_low<true, kOffI, 1>(x, G);
-    layer_low<true, kOffI, 2>(x, G);
-    exchange<true>(x, area, g, l);
-    layer_top<true, kOffI, 3>(x);
-    layer_top<true, kOffI, 4>(x);
-    layer_top<true, kOffI, 5>(x);
-    fused_top<kOffI, kOffF>(x);
-    layer_top<false, kOffF, 5>(x);
-    layer_top<false, kOffF, 4>(x);
-    layer_top<false, kOffF, 3>(x);
-    exchange<false>(x, area, g, l);
-    layer_low<false, kOffF, 2>(x, G);
-    layer_low<false, kOffF, 1>(x, G);
-    layer_low<false, kOffF, 0>(x, G);
-
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        transpose8(x[r], xm);
-        pin8(x[r]);
-        bs_fence();
-    }
-#endif
-    uint8_t* base = reinterpret_cast<uint8_t*>(a.out_base + col) + int64_t(g << 4) * a.out_stride;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        uint8_t* p = base + int64_t(r) * a.out_stride;
+    for (int r = R0; r < R0 + 8; ++r) {
+        uint8_t* p = T.out + int64_t(r) * T.out_stride;
         v4u v0, v1;
         v0.x = x[r][0], v0.y = x[r][1], v0.z = x[r][2], v0.w = x[r][3];
         v1.x = x[r][4], v1.y = x[r][5], v1.z = x[r][6], v1.w = x[r][7];
 #ifdef ABL_MEM
-        uint32_t acc = v0.x ^ v0.y ^ v0.z ^ v0.w ^ v1.x ^ v1.y ^ v1.z ^ v1.w;
-        if (acc == 0x12345679u && rem == 7u) *gptr<uint32_t>(p) = acc;  // keep the values live
+        const uint32_t acc = v0.x ^ v0.y ^ v0.z ^ v0.w ^ v1.x ^ v1.y ^ v1.z ^ v1.w;
+        if (acc == 0x12345679u && T.in_stride == 7) *gptr<uint32_t>(p) = acc;  // keep the values live
         continue;
 #endif
-        if (live0) *gptr<v4u>(p + o0) = v0;
-        if (live1) *gptr<v4u>(p + o1) = v1;
+        // A segment past the piece's end was loaded from segment 0 of the
+        // strip (always inside: pieces are multiples of 64 bytes), and the
+        // transform is column by column, so it holds segment 0's output: it is
+        // stored there, the same bytes lane 8 g writes (no branch per store).
+        *gptr<v4u>(p + T.l0) = v0;
+        *gptr<v4u>(p + T.l1) = v1;
+    }
+}
+template <int R0>
+LDEV void transpose_half(Reg& x, const XMasks& xm) {
+#pragma unroll
+    for (int r = R0; r < R0 + 8; ++r) {
+        transpose8(x[r], xm);
+        pin8(x[r]);
+        bs_fence();
     }
 }
 
-// Persistent waves: the grid fills the GPU once (kBsWaves waves a workgroup,
-// one workgroup a CU at two waves per SIMD) and wave i codes tiles i, i + n,
-// ... (tile = object * strips + strip).  Every tile is load -> ~10 us of
-// butterflies -> store; the two waves a SIMD holds start half a tile apart
-// (the waves kBsWaves / 2 .. kBsWaves - 1 of a workgroup, placed on the SIMDs
-// after the first half, sleep first), so that one computes while the other's
-// loads and stores are in flight, instead of both waiting on HBM at the same
-// time tile after tile.
+// Persistent waves: the grid fills the GPU once (kBsBlocksPerCu workgroups of
+// kBsWaves independent waves a CU) and wave i codes tiles i, i + n, ... (tile =
+// object * strips + strip).  A tile is software-pipelined in halves: the low
+// layers (0-2) pair registers r and r ^ 1, 2, 4 only, so pieces 0-7 and 8-15 of
+// layout 0 are independent there.  The last FFT layers, transposes and stores
+// of half 0 run, then the next tile's half-0 loads are issued into the freed
+// registers while half 1 computes; at the top of the next tile half 1's loads
+// are in flight while half 0 transposes and runs its IFFT layers.
 #ifndef LAMD_BS_STAGGER
 #define LAMD_BS_STAGGER 0  // s_sleep 127 (8128 cycles) steps of the second wave of a SIMD (measured: 1, 2, 4 slower)
 #endif
 template <int kForm>
 __global__ void __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(LAMD_BS_OCC, LAMD_BS_OCC)))
 k_ff8_bs_slab(Ff8SlabBatch b, uint32_t count, uint32_t strips) {
+    constexpr int kOffI = kForm == kFormDenseDec ? -1 : 127;  // IFFT skew base
+    constexpr int kOffF = kForm == kFormDenseDec ? 127 : -1;  // FFT skew base
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const unsigned wave = threadIdx.x >> 6;
     const unsigned n = gridDim.x * kBsWaves, total = count * strips;
     uint8_t* const area = reinterpret_cast<uint8_t*>(lds + wave * kBsAreaDw);
     unsigned t = blockIdx.x * kBsWaves + wave;
+    if (t >= total) return;  // wave-uniform; waves share nothing
     if (wave >= kBsWaves / 2 && t + n < total)
         for (int i = 0; i < LAMD_BS_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
-    for (; t < total; t += n) {
-        const unsigned obj = t / strips, strip = t - obj * strips;
-        ff8_bs<kForm>(Ff8SlabView(b, obj), area, strip);
+    const unsigned lane = threadIdx.x & 63u, g = lane >> 3, l = lane & 7u;
+    const uint32_t G[3] = {(g & 1u) ? ~0u : 0u, (g & 2u) ? ~0u : 0u, (g & 4u) ? ~0u : 0u};
+    const XMasks xm;
+    Reg x;
+    BsTile cur = bs_tile(b, t, strips, g, l);
+    load_half<0>(x, cur);
+    load_half<8>(x, cur);
+    for (;;) {
+#ifndef ABL_ARITH
+        transpose_half<0>(x, xm);
+        layer_low<true, kOffI, 0, 0>(x, G);
+        layer_low<true, kOffI, 1, 0>(x, G);
+        layer_low<true, kOffI, 2, 0>(x, G);
+        transpose_half<8>(x, xm);
+        layer_low<true, kOffI, 0, 8>(x, G);
+        layer_low<true, kOffI, 1, 8>(x, G);
+        layer_low<true, kOffI, 2, 8>(x, G);
+        exchange<true>(x, area, g, l);
+        layer_top<true, kOffI, 3>(x);
+        layer_top<true, kOffI, 4>(x);
+        layer_top<true, kOffI, 5>(x);
+        fused_top<kOffI, kOffF>(x);
+        layer_top<false, kOffF, 5>(x);
+        layer_top<false, kOffF, 4>(x);
+        layer_top<false, kOffF, 3>(x);
+        exchange<false>(x, area, g, l);
+#endif
+        const unsigned tn = t + n;
+        const bool more = tn < total;
+        const BsTile nxt = bs_tile(b, more ? tn : t, strips, g, l);
+#ifndef ABL_ARITH
+        layer_low<false, kOffF, 2, 0>(x, G);
+        layer_low<false, kOffF, 1, 0>(x, G);
+        layer_low<false, kOffF, 0, 0>(x, G);
+        transpose_half<0>(x, xm);
+#endif
+        store_half<0>(x, cur);
+        if (more) load_half<0>(x, nxt);
+#ifndef ABL_ARITH
+        layer_low<false, kOffF, 2, 8>(x, G);
+        layer_low<false, kOffF, 1, 8>(x, G);
+        layer_low<false, kOffF, 0, 8>(x, G);
+        transpose_half<8>(x, xm);
+#endif
+        store_half<8>(x, cur);
+        if (!more) break;
+        load_half<8>(x, nxt);
+        t = tn;
+        cur = nxt;
     }
 }
 

@@ -30,7 +30,7 @@ fixed as N grows).  With N > 1, rank 0 also times the whole object alone on
 its GPU in the same run, so the line carries the 1-GPU time of that object.
 
 Roofline: the dominant kernel of the headline's timed region (batch mode: the
-encode-batch or decode-batch launch, k_ff8_enc_slab, whichever is longer) is
+encode-batch or decode-batch launch, k_ff8_bs_slab, whichever is longer) is
 timed alone with HIP events on the stream it runs on (back-to-back launches
 queued behind a spin kernel); achieved = algorithmic bytes per launch (objects
 x ((K + R) * B encode, (K_surv + lost) * B decode)) / mean
@@ -277,7 +277,7 @@ def main():
         achieved = algo / t_kernel / 1e9
         s_kind, s_algo, s_t = head["single_dominant"]
         s_traffic = pmc_traffic(s_kind, k, r, nbytes, 1)
-        kname = ("k_ff8_enc_slab<7,4,false,%d>: one %d-object batch launch (%s)"
+        kname = ("k_ff8_bs_slab<%d>: one %d-object batch launch (bit-sliced tile, %s)"
                  % (2 if kind == "decode" else 1, head["launch_objects"], "full-loss decode form" if kind == "decode"
                     else "dense encode form")) if batch else kind
         out = {

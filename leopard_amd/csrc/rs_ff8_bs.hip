@@ -61,6 +61,16 @@ constexpr unsigned kBsAreaDw = (128 + 8) * 8 * 2;  // LDS dwords per wave: 136 r
 LDEV void bs_fence() {
     if constexpr (LAMD_BS_SCHED) __builtin_amdgcn_sched_barrier(0);
 }
+#ifndef LAMD_BS_XFENCE
+#define LAMD_BS_XFENCE 1  // transposes between scheduling barriers
+#endif
+#ifndef LAMD_BS_BFENCE
+#define LAMD_BS_BFENCE 1  // butterflies between scheduling barriers
+#endif
+template <int N>
+LDEV void bs_fence_every(int i) {
+    if ((i + 1) % N == 0) bs_fence();
+}
 
 // ---------------------------------------------------------- bit planes -----
 
@@ -225,7 +235,7 @@ LDEV void layer_low(Reg& x, const uint32_t (&G)[3]) {
             }
             pin8(a);
             pin8(b);
-            bs_fence();
+            bs_fence_every<LAMD_BS_BFENCE>(int((r >> (L + 1)) << L | (r & (half - 1))));
         }
     });
 }
@@ -250,7 +260,7 @@ LDEV void layer_top(Reg& x) {
             }
             pin8(a);
             pin8(b);
-            bs_fence();
+            bs_fence_every<LAMD_BS_BFENCE>(int((r >> (L - 2)) << (L - 3) | (r & (half - 1))));
         }
     });
 }
@@ -271,7 +281,7 @@ LDEV void fused_top(Reg& x) {
         for (int k = 0; k < 8; ++k) b[k] ^= a[k];
         pin8(a);
         pin8(b);
-        bs_fence();
+        bs_fence_every<LAMD_BS_BFENCE>(int(r));
     });
 }
 
@@ -393,7 +403,7 @@ LDEV void transpose_half(Reg& x, const XMasks& xm) {
     for (int r = R0; r < R0 + 8; ++r) {
         transpose8(x[r], xm);
         pin8(x[r]);
-        bs_fence();
+        bs_fence_every<LAMD_BS_XFENCE>(r);
     }
 }
 

@@ -587,7 +587,8 @@ def configs4_sharded(args, leo, torch, device, barrier, rank, world, max_over_ra
     for _ in range(nsteps):
         step(off, size)
     torch.cuda.synchronize()
-    el = max_over_ranks(time.perf_counter() - t0)
+    el_local = time.perf_counter() - t0
+    el = max_over_ranks(el_local)
     n1_ms = None
     if world > 1:  # the same object on one GPU (rank 0 alone) for the strong-scaling ratio
         barrier()
@@ -643,6 +644,17 @@ def configs4_sharded(args, leo, torch, device, barrier, rank, world, max_over_ra
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(algo1 / cms / 1e6 / HBM_PEAK_GBPS, 4),
                      "algorithmic_bytes": algo1, "traffic": t.get("bytes"), "traffic_source": t.get("source")}
     res["per_call"] = per
+    # every rank's own step time and slice-kernel times (where strong scaling is lost:
+    # a slow rank, or slices whose kernels do not shrink with the columns)
+    mine = {"rank": rank, "columns": [off, size], "ms_per_step": round(el_local / nsteps * 1e3, 3),
+            "encode_ms": per["encode"]["ms"], "decode_ms": per["decode"]["ms"]}
+    if world > 1:
+        import torch.distributed as dist
+        allr = [None] * world
+        dist.all_gather_object(allr, mine)
+        res["per_rank"] = allr
+    else:
+        res["per_rank"] = [mine]
     if n1_ms is not None:
         res["one_gpu_ms_per_step"] = round(n1_ms, 3)
         res["speedup_vs_one_gpu"] = round(n1_ms / ms, 3)

@@ -24,8 +24,9 @@ def _run(args, timeout=180):
                           text=True, timeout=timeout)
 
 
-@pytest.mark.parametrize("n", [2, 3])
+@pytest.mark.parametrize("n", [2, 3, 8])
 def test_bench_launches_n_ranks(n):
+    """N = 8 is the driver's SCALE run (8 ranks, one per GPU of a node)."""
     p = _run(["--gpus", str(n), "--stub"])
     assert p.returncode == 0, p.stderr[-2000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]

@@ -2172,11 +2172,29 @@ LeopardResult encode_batch16(int dev, unsigned count, uint64_t bytes, unsigned K
 }
 
 // Decoder: objects in chunks of kDec16Slots (each object's erasure pattern
-// holds a decoder-state slot for the chunk), a U slab per object, at most
-// kBatch16SlabBytes of slabs a chunk.  Only for pieces under kOnePassMinBytes:
-// larger pieces decode object by object in the one-pass form (no slab), whose
-// single-object grid already fills the GPU.
+// holds a decoder-state slot for the chunk).  At most kDecOneNZ output tiles:
+// the one-pass kernel over every object of a chunk in one grid (no
+// intermediate).  Otherwise the two passes with a U slab per object, at most
+// kBatch16SlabBytes of slabs a chunk, and only for pieces under
+// kOnePassMinBytes (larger pieces decode object by object).
 constexpr uint64_t kBatch16SlabBytes = 256ull << 20;
+// One-pass batch when its grid (16-unit strips x objects) gives every CU at
+// least kBatch16OneWgsPerCu workgroups; below that the two-pass form's grids
+// (one workgroup per strip and tile) keep more SIMDs busy (16 objects of
+// 2560-byte pieces: 9.56 vs 8.07 us per object, profiles/r05_v2).
+// LEO_AMD_DEC16_BATCH_ONE=0/1 forces either form in experiment builds.
+constexpr uint64_t kBatch16OneWgsPerCu = 4;
+bool batch16_one_pass(unsigned count, uint64_t bytes) {
+#if LAMD_EXPERIMENT_ENV
+    static const int force = [] {
+        const char* e = std::getenv("LEO_AMD_DEC16_BATCH_ONE");
+        return e ? (e[0] == '1' ? 1 : 0) : -1;
+    }();
+    if (force >= 0) return force == 1;
+#endif
+    const uint64_t wgs = (bytes / 8 + 15) / 16 * count;
+    return wgs >= kBatch16OneWgsPerCu * 256;
+}
 LeopardResult decode_batch16(int dev, unsigned count, uint64_t bytes, unsigned K, unsigned R,
                              const void* const* const* orig, const void* const* const* rec, void** const* work) {
     DeviceGuard guard(dev);
@@ -2187,9 +2205,12 @@ LeopardResult decode_batch16(int dev, unsigned count, uint64_t bytes, unsigned K
     const unsigned m = next_pow2(R), n = next_pow2(m + K), Tn = log2u(n);
     const unsigned ntiles_in = (m + K + (1u << kLoBits) - 1) >> kLoBits;
     const unsigned tile0 = m >> kLoBits, nout = ((m + K - 1) >> kLoBits) - tile0 + 1;
-    const uint64_t slab = (uint64_t(ntiles_in) << kLoBits) * bytes;  // U of one object
-    const unsigned per_chunk = unsigned(std::max<uint64_t>(1, std::min<uint64_t>(Workspace::kDec16Slots,
-                                                                                  kBatch16SlabBytes / slab)));
+    // one pass (round 5): no U slab, one grid (strips, objects); two passes otherwise
+    const bool one = decode16_one_supported(nout) && batch16_one_pass(count, bytes);
+    const uint64_t slab = one ? 0 : (uint64_t(ntiles_in) << kLoBits) * bytes;  // U of one object
+    const unsigned per_chunk =
+        one ? Workspace::kDec16Slots
+            : unsigned(std::max<uint64_t>(1, std::min<uint64_t>(Workspace::kDec16Slots, kBatch16SlabBytes / slab)));
     for (unsigned o0 = 0; o0 < count; o0 += per_chunk) {
         const unsigned nb = std::min(per_chunk, count - o0);
         ++ws.dec16_call;
@@ -2216,7 +2237,10 @@ LeopardResult decode_batch16(int dev, unsigned count, uint64_t bytes, unsigned K
             args[o].a_out = args[o].a_in = PieceMap{nullptr, ws.dbuf + table_bytes + args_bytes + o * slab, bytes, 0};
         DecArgs* dargs = reinterpret_cast<DecArgs*>(ws.dbuf + table_bytes);
         if ((r = ws.upload(dargs, args.data(), nb * sizeof(DecArgs), c.s)) != Leopard_Success) return r;
-        HIP_OK(launch_decode16_small_batch(dargs, nb, bytes / 8, ntiles_in, nout, c.s), "batch decode kernels");
+        if (one)
+            HIP_OK(launch_decode16_one_batch(dargs, nb, bytes / 8, c.s), "batch decode kernel");
+        else
+            HIP_OK(launch_decode16_small_batch(dargs, nb, bytes / 8, ntiles_in, nout, c.s), "batch decode kernels");
     }
     return finish(c, false);
 }
@@ -2372,7 +2396,13 @@ LeopardResult decode_batch(unsigned count, uint64_t bytes, unsigned K, unsigned 
                 for (unsigned i = 0; i < K && on_dev; ++i)
                     if (!orig[o][i]) on_dev = rc.on(work[o][i], bytes, d16);
             }
-            if (on_dev && bytes < kOnePassMinBytes) return decode_batch16(d16, count, bytes, K, R, orig, rec, work);
+            const unsigned m16 = next_pow2(R);
+            const unsigned nout16 = ((m16 + K - 1) >> kLoBits) - (m16 >> kLoBits) + 1;
+            // the two-pass batch keeps a U slab per object: only for pieces under
+            // kOnePassMinBytes, where a single object does not fill the GPU
+            if (on_dev && ((decode16_one_supported(nout16) && batch16_one_pass(count, bytes)) ||
+                           bytes < kOnePassMinBytes))
+                return decode_batch16(d16, count, bytes, K, R, orig, rec, work);
         }
     }
     for (unsigned o = 0; o < count; ++o) {

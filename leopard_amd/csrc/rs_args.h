@@ -179,6 +179,7 @@ hipError_t launch_decode16_small_batch(const DecArgs* objs, unsigned count, uint
 // accumulators, then low FFT + reveal per output tile) when nout is small
 bool decode16_one_supported(unsigned nout);
 hipError_t launch_decode16_one(const DecArgs& a, hipStream_t s);
+hipError_t launch_decode16_one_batch(const DecArgs* objs, unsigned count, uint64_t nunits, hipStream_t s);
 hipError_t launch_ff8_encode(unsigned T, const Ff8EncArgs& a, hipStream_t s);
 hipError_t launch_ff8_decode(unsigned T, const Ff8DecArgs& a, hipStream_t s);
 hipError_t launch_error_locator8(const El8Args& a, unsigned count, hipStream_t s);

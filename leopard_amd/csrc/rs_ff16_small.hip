@@ -621,7 +621,7 @@ constexpr size_t one_lds_dwords() {
     return one_xch_dwords<R, LW>() + 2 * tab16_set_dwords(8) + 2 * 256;
 }
 template <int R, int LW, int NZ>
-__global__ void __launch_bounds__((threads_n<8, R, LW>()), LAMD_DEC16_ONE_WAVES) k_dec16n_one(DecArgs a) {
+LDEV void dec16n_one(const DecArgs& a) {
     if constexpr ((LAMD_ABLATE & 16) != 0) return;
     constexpr int T = 8, G = lg_bits(LW);
     using TL = Tile<FF16, T, R, 1, LW, 0, G>;
@@ -868,6 +868,19 @@ __global__ void __launch_bounds__((threads_n<8, R, LW>()), LAMD_DEC16_ONE_WAVES)
 #undef STAMP1
 
 template <int R, int LW, int NZ>
+__global__ void __launch_bounds__((threads_n<8, R, LW>()), LAMD_DEC16_ONE_WAVES) k_dec16n_one(DecArgs a) {
+    dec16n_one<R, LW, NZ>(a);
+}
+// Batches (round 5): object blockIdx.y of an array of argument blocks in device
+// memory (read through the scalar cache like the kernel arguments), each with
+// its own decoder-state slot -- no U slab for batches either.
+template <int R, int LW, int NZ>
+__global__ void __launch_bounds__((threads_n<8, R, LW>()), LAMD_DEC16_ONE_WAVES)
+k_dec16n_one_batch(const DecArgs* __restrict__ objs) {
+    dec16n_one<R, LW, NZ>(objs[blockIdx.y]);
+}
+
+template <int R, int LW, int NZ>
 __global__ void __launch_bounds__((threads_n<8, R, LW>()), LAMD_DEC16N_FIN_WAVES) k_dec16n_fin(DecArgs a) {
     dec16n_fin_body<R, LW, NZ>(a);
 }
@@ -983,6 +996,17 @@ hipError_t launch_decode16_one(const DecArgs& a, hipStream_t s) {
     const unsigned strips = unsigned((a.nunits + 15) / 16);
     return launch16n(&k_dec16n_one<kDecOneR, 16, kDecOneNZ>, dim3(strips), threads_n<8, kDecOneR, 16>(), kDecOneLds16,
                      a, s);
+}
+// the one-pass form over `count` objects of one shape (nout <= kDecOneNZ)
+hipError_t launch_decode16_one_batch(const DecArgs* objs, unsigned count, uint64_t nunits, hipStream_t s) {
+    const unsigned strips = unsigned((nunits + 15) / 16);
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dec16n_one_batch<kDecOneR, 16, kDecOneNZ>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, int(kDecOneLds16));
+    if (e != hipSuccess) return e;
+    const DecArgs* arg = objs;
+    void* params[] = {&arg};
+    return hipLaunchKernel(reinterpret_cast<const void*>(&k_dec16n_one_batch<kDecOneR, 16, kDecOneNZ>),
+                           dim3(strips, count), dim3(threads_n<8, kDecOneR, 16>()), params, kDecOneLds16, s);
 }
 // both passes over `count` objects of one shape (same nlo, nout, column count)
 hipError_t launch_decode16_small_batch(const DecArgs* objs, unsigned count, uint64_t nunits, unsigned nlo,

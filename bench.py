@@ -10,9 +10,11 @@ bytes, GF(2^8).  One *step* = one pass over OBJECTS independent objects
 (default 64, a storage node's stripes): each is encoded and then decoded with
 every original lost (the benchmark's worst case, rebuilt from the 128 recovery
 pieces).  Default mode "batch": the objects go out in launches of
---launch-objects (default 16) through the leo_amd_encode_batch /
-leo_amd_decode_batch extension (one kernel per 16 objects), consecutive launch
-pairs alternating over 2 streams; the line records mode and objects per launch.
+--launch-objects (default 64: the whole step, one encode and one decode
+launch) through the leo_amd_encode_batch / leo_amd_decode_batch extension,
+consecutive launch pairs alternating over 2 streams; the line records mode and
+objects per launch (16 / 32 / 64 objects per launch measured 1127-1140 /
+1151-1170 / 1181-1193 GB/s, profiles/r05_v2/headline_launch_sweep.txt).
 `modes` also carries the drop-in comparable figures through the reference
 C ABI: "calls_in_flight" (leo_encode + leo_decode per object, 3 streams in
 flight, async device pointers) and "serial" (one stream, each call waiting for
@@ -83,7 +85,7 @@ def parse():
     ap.add_argument("--R", type=int, default=128)
     ap.add_argument("--bytes", type=int, default=65536)
     ap.add_argument("--objects", type=int, default=64, help="independent objects per step")
-    ap.add_argument("--launch-objects", type=int, default=16,
+    ap.add_argument("--launch-objects", type=int, default=64,
                     help="batch mode: objects per leo_amd_*_batch launch (a step is objects / launch-objects launches)")
     ap.add_argument("--sets", type=int, default=0, help="buffer sets rotated (0 = enough for >512 MiB)")
     ap.add_argument("--streams", type=int, default=3,

@@ -15,8 +15,8 @@ cat $OUT/prof_bench.json
 find $OUT/prof -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
 KB_ARGS="${PMC_ARGS:-128 128 65536}" bash tools/pmc.sh FETCH_SIZE WRITE_SIZE || exit 1
 python3 tools/pmc_traffic.py ${PMC_ARGS:-128 128 65536} gpurun_out/pmc1 gpurun_out/pmc2 > $OUT/pmc_traffic.json && cat $OUT/pmc_traffic.json
-# the batch kernels of the headline (16 objects per launch)
+# the batch kernels of the headline (LAUNCH_OBJ objects per launch, the bench default 64)
 rm -rf gpurun_out/pmc1 gpurun_out/pmc2
-PMC_TOOL=bbench KB_ARGS="${PMC_ARGS:-128 128 65536} 16" bash tools/pmc.sh FETCH_SIZE WRITE_SIZE || exit 1
-python3 tools/pmc_traffic.py --objects 16 ${PMC_ARGS:-128 128 65536} gpurun_out/pmc1 gpurun_out/pmc2 > $OUT/pmc_traffic_batch.json && cat $OUT/pmc_traffic_batch.json
+PMC_TOOL=bbench KB_ARGS="${PMC_ARGS:-128 128 65536} ${LAUNCH_OBJ:-64}" bash tools/pmc.sh FETCH_SIZE WRITE_SIZE || exit 1
+python3 tools/pmc_traffic.py --objects ${LAUNCH_OBJ:-64} ${PMC_ARGS:-128 128 65536} gpurun_out/pmc1 gpurun_out/pmc2 > $OUT/pmc_traffic_batch.json && cat $OUT/pmc_traffic_batch.json
 rm -rf gpurun_out/pmc1 gpurun_out/pmc2 $OUT/prof  # raw passes and traces: summarised above

@@ -31,12 +31,17 @@ leo_amd_encode_slice / leo_amd_decode_slice on its B/N columns of every piece
 fixed as N grows).  With N > 1, rank 0 also times the whole object alone on
 its GPU in the same run, so the line carries the 1-GPU time of that object.
 
-Roofline: the dominant kernel of the headline's timed region (batch mode: the
-encode-batch or decode-batch launch, k_ff8_bs_slab, whichever is longer) is
-timed alone with HIP events on the stream it runs on (back-to-back launches
-queued behind a spin kernel); achieved = algorithmic bytes per launch (objects
-x ((K + R) * B encode, (K_surv + lost) * B decode)) / mean
-launch duration, against the 8 TB/s HBM3E peak.  traffic = HBM bytes per
+Roofline: the kernel of the headline's timed region (batch mode: the
+encode-batch and decode-batch launches, k_ff8_bs_slab<1> / <2>), timed inside
+that region with HIP events recorded right before and after every launch on
+its stream.  Consecutive launch pairs on 2 streams overlap (a launch's ramp-up
+runs under the previous one's drain), so the launch time is the GPU time per
+launch over the region, (last post-launch event - first pre-launch event) /
+launches ("launch_us"); each launch's own pre->post span (= rocprofv3's kernel
+duration, which counts the overlapped time twice) is reported beside it.
+achieved = algorithmic bytes per launch (objects x ((K + R) * B encode,
+(K_surv + lost) * B decode)) / launch_us, against the 8 TB/s
+HBM3E peak.  traffic = HBM bytes per
 launch from the committed rocprofv3 PMC pass (tools/pmc_traffic.py), when
 present for this workload.  roofline.single_call carries the same figures for
 one leo_encode / leo_decode call (the plain drop-in caller's kernel).
@@ -279,9 +284,8 @@ def main():
         achieved = algo / t_kernel / 1e9
         s_kind, s_algo, s_t = head["single_dominant"]
         s_traffic = pmc_traffic(s_kind, k, r, nbytes, 1)
-        kname = ("k_ff8_bs_slab<%d>: one %d-object batch launch (bit-sliced tile, %s)"
-                 % (2 if kind == "decode" else 1, head["launch_objects"], "full-loss decode form" if kind == "decode"
-                    else "dense encode form")) if batch else kind
+        kname = ("k_ff8_bs_slab<1> / <2>: %d-object encode-batch / decode-batch launches (bit-sliced tile; "
+                 "dense encode form / full-loss decode form)" % head["launch_objects"]) if batch else kind
         out = {
             "metric": "device-resident encode+decode GB/s (input bytes/s) at 128+128 and 32768+32768 pieces",
             "value": head["value"],
@@ -332,8 +336,13 @@ def main():
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "traffic": traffic.get("bytes"), "traffic_source": traffic.get("source"),
                          "algorithmic_bytes_per_launch": algo, "launch_us": round(t_kernel * 1e6, 3),
-                         "batch_encode_us": round(head["tb_enc"] * 1e6, 3),
-                         "batch_decode_us": round(head["tb_dec"] * 1e6, 3),
+                         "launch_time": ("busy: GPU time per launch over the timed region, (last post-launch "
+                                         "event - first pre-launch event) / launches; span: one launch's own "
+                                         "pre->post event interval, the rocprofv3 kernel-trace duration, which "
+                                         "counts the time it overlaps the neighbouring launch on the other "
+                                         "stream" if batch else "back-to-back single calls behind a spin kernel"),
+                         **({"launch_span_encode_us": round(head["span_enc"] * 1e6, 3),
+                             "launch_span_decode_us": round(head["span_dec"] * 1e6, 3)} if batch else {}),
                          # per-config fractions as scalars (the driver's record keeps scalars only)
                          "single_call_us": round(s_t * 1e6, 3),
                          "single_call_frac": round(s_algo / s_t / 1e9 / HBM_PEAK_GBPS, 4),
@@ -437,22 +446,36 @@ def headline(args, leo, torch, device, barrier, world, max_over_ranks):
     bstreams = [stream] + [torch.cuda.Stream(device) for _ in range(max(1, args.batch_streams) - 1)]
     groups = -(-args.objects // lobj)
 
-    def run_batches(nsteps, _ns):
+    # ev (timed region only): four events per launch pair, on the pair's stream
+    # right before and after each of its two launches.
+    def run_batches(nsteps, _ns, ev=None):
         for s in range(nsteps):
             for g in range(groups):
                 j = s * groups + g
                 cnt = min(lobj, args.objects - g * lobj)
-                leo.set_stream(bstreams[j % len(bstreams)].cuda_stream)
+                st = bstreams[j % len(bstreams)]
+                leo.set_stream(st.cuda_stream)
                 bo, bw, bn, br, bd = batches[(s * args.objects // lobj + g) % nbatches]
-                if (lib.leo_amd_encode_batch(cnt, nbytes, k, r, sets.enc_wc, bo, bw) != 0 or
-                        lib.leo_amd_decode_batch(cnt, nbytes, k, r, sets.dec_wc, bn, br, bd) != 0):
+                if ev is not None:
+                    ev[4 * j].record(st)
+                rc = lib.leo_amd_encode_batch(cnt, nbytes, k, r, sets.enc_wc, bo, bw)
+                if ev is not None:
+                    ev[4 * j + 1].record(st)
+                    ev[4 * j + 2].record(st)
+                rc = rc or lib.leo_amd_decode_batch(cnt, nbytes, k, r, sets.dec_wc, bn, br, bd)
+                if ev is not None:
+                    ev[4 * j + 3].record(st)
+                if rc != 0:
                     raise RuntimeError(leo.last_error())
 
-    def timed(run, ns):
+    def timed(run, ns, ev=None):
         run(args.warmup, ns)
         barrier()
         t0 = time.perf_counter()
-        run(args.steps, ns)
+        if ev is None:
+            run(args.steps, ns)
+        else:
+            run(args.steps, ns, ev)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         el = max_over_ranks(t1 - t0)
@@ -470,7 +493,9 @@ def headline(args, leo, torch, device, barrier, world, max_over_ranks):
         assert torch.equal(sets.dec_work[i][:k], sets.orig[i]), "batch decode mismatch"
     elapsed_calls = timed(run_calls, nstreams)
     elapsed_serial = timed(run_calls, 1)
-    elapsed_batch = timed(run_batches, 1)
+    # the headline's launch events: allocated before the timed region, read after it
+    batch_ev = [torch.cuda.Event(enable_timing=True) for _ in range(4 * args.steps * groups)]
+    elapsed_batch = timed(run_batches, 1, batch_ev)
     elapsed = elapsed_batch if args.mode == "batch" else elapsed_calls
     leo.set_stream(stream.cuda_stream)
 
@@ -498,32 +523,25 @@ def headline(args, leo, torch, device, barrier, world, max_over_ranks):
     algo_dec = (r + k) * nbytes  # R surviving pieces read + K lost originals written (full loss)
     dominant = ("decode", algo_dec, t_dec) if t_dec >= t_enc else ("encode", algo_enc, t_enc)
 
-    # The batch mode's kernels (the headline's timed region: one encode-batch and
-    # one decode-batch launch per step), timed the same way: back-to-back launches
-    # behind a spin kernel on the launch stream, time / n = mean launch duration.
-    def time_batch(decode, n=20):
-        leo.set_stream(stream.cuda_stream)
-
-        def launch(j):
-            bo, bw, bn, br, bd = batches[j % nbatches]
-            rc = (lib.leo_amd_decode_batch(lobj, nbytes, k, r, sets.dec_wc, bn, br, bd) if decode
-                  else lib.leo_amd_encode_batch(lobj, nbytes, k, r, sets.enc_wc, bo, bw))
-            if rc != 0:
-                raise RuntimeError(leo.last_error())
-        for j in range(3):
-            launch(j)
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        torch.cuda._sleep(50_000_000)
-        e0.record(stream)
-        for j in range(n):
-            launch(j)
-        e1.record(stream)
-        torch.cuda.synchronize()
-        return e0.elapsed_time(e1) / 1e3 / n
-
-    tb_enc, tb_dec = time_batch(False), time_batch(True)
-    algo_batch = lobj * (k + r) * nbytes
+    # The batch mode's kernels, timed inside the headline's timed region itself
+    # from the events recorded right before and after every encode-batch and
+    # decode-batch launch on its stream (one kernel per launch on this path):
+    #  - span: a launch's own pre->post interval (what rocprofv3's kernel trace
+    #    reports as its duration).  With --batch-streams 2 consecutive launches
+    #    overlap (one launch's ramp-up runs under the previous one's drain), so a
+    #    span counts the overlapped time in both launches;
+    #  - busy: GPU time per launch = (last post - first pre) / launches; equal to
+    #    span + gap with one stream, and the time each launch adds to the GPU's
+    #    busy time when they overlap (any idle GPU time counts against it).
+    # tb_* (the roofline's launch time) is busy; spans are reported beside it.
+    npairs = args.steps * groups
+    span_enc = sum(batch_ev[4 * j].elapsed_time(batch_ev[4 * j + 1]) for j in range(npairs)) / npairs / 1e3
+    span_dec = sum(batch_ev[4 * j + 2].elapsed_time(batch_ev[4 * j + 3]) for j in range(npairs)) / npairs / 1e3
+    last = max(batch_ev[0].elapsed_time(batch_ev[4 * j + 3]) for j in range(max(0, npairs - 4), npairs))
+    busy = last / (2 * npairs) / 1e3
+    tb_enc = tb_dec = busy
+    del batch_ev
+    algo_batch = args.objects * (k + r) * nbytes / groups  # mean objects per launch x bytes per object
     batch_dominant = (("decode", algo_batch, tb_dec) if tb_dec >= tb_enc else ("encode", algo_batch, tb_enc))
     if args.mode == "batch":
         dominant, single_dominant = batch_dominant, dominant
@@ -545,7 +563,8 @@ def headline(args, leo, torch, device, barrier, world, max_over_ranks):
                                                       f"in flight on {nstreams} streams"),
                "serial": rate(elapsed_serial, "one leo_encode + leo_decode per object on one stream: each call "
                                               "waits for the previous (a plain drop-in caller)")},
-           "t_enc": t_enc, "t_dec": t_dec, "tb_enc": tb_enc, "tb_dec": tb_dec, "dominant": dominant,
+           "t_enc": t_enc, "t_dec": t_dec, "tb_enc": tb_enc, "tb_dec": tb_dec,
+           "span_enc": span_enc, "span_dec": span_dec, "dominant": dominant,
            "single_dominant": single_dominant, "sets": sets.n, "streams": nstreams, "launch_objects": lobj}
     del sets
     torch.cuda.empty_cache()

@@ -10,9 +10,10 @@ OUT=${OUT:-gpurun_out/round}
 rm -rf $OUT; mkdir -p $OUT
 timeout -k 10 600 python3 bench.py ${BENCH_ARGS:-} > $OUT/bench.json 2> $OUT/bench.err || { tail -30 $OUT/bench.err; exit 1; }
 cat $OUT/bench.json
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-host --no-secondary --streams 1 --batch-streams 1 ${BENCH_ARGS:-} > $OUT/prof_bench.json 2> $OUT/prof.err || { tail -20 $OUT/prof.err; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-host --no-secondary ${BENCH_ARGS:-} > $OUT/prof_bench.json 2> $OUT/prof.err || { tail -20 $OUT/prof.err; exit 1; }
 cat $OUT/prof_bench.json
 find $OUT/prof -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
+python3 tools/trace_summary.py $(find $OUT/prof -name "*kernel_trace.csv") > $OUT/trace_summary.txt && grep "run of" $OUT/trace_summary.txt
 KB_ARGS="${PMC_ARGS:-128 128 65536}" bash tools/pmc.sh FETCH_SIZE WRITE_SIZE || exit 1
 python3 tools/pmc_traffic.py ${PMC_ARGS:-128 128 65536} gpurun_out/pmc1 gpurun_out/pmc2 > $OUT/pmc_traffic.json && cat $OUT/pmc_traffic.json
 # the batch kernels of the headline (LAUNCH_OBJ objects per launch, the bench default 64)

@@ -252,10 +252,29 @@ struct VecT<2> { using type = v2u; };
 template <>
 struct VecT<4> { using type = v4u; };
 
+// Piece loads / stores, plain or nontemporal (nt: streamed past the caches'
+// retention).  nt is the default where it was measured faster: the GF(2^8)
+// dense tiles (bit-sliced batch +4%, single call 9.9 -> 8.8 us); the GF(2^16)
+// passes were equal or slower with it (profiles/r05_v6/ntall_ab.txt), so the
+// unit helpers below stay plain unless an experiment build sets LAMD_NT_IO.
+#ifndef LAMD_NT_IO
+#define LAMD_NT_IO 0
+#endif
+template <class V, bool kNt = LAMD_NT_IO != 0>
+LDEV V gld(const uint8_t* p) {
+    if constexpr (kNt) return __builtin_nontemporal_load(gptr<const V>(p));
+    else return *gptr<const V>(p);
+}
+template <class V, bool kNt = LAMD_NT_IO != 0>
+LDEV void gst(uint8_t* p, const V& v) {
+    if constexpr (kNt) __builtin_nontemporal_store(v, gptr<V>(p));
+    else *gptr<V>(p) = v;
+}
+
 template <int C>
 LDEV void vload(uint32_t* dst, const uint8_t* src) {
     using V = typename VecT<C>::type;
-    const V v = *gptr<const V>(src);
+    const V v = gld<V>(src);
     if constexpr (C == 1) dst[0] = v;
     else if constexpr (C == 2) { dst[0] = v.x; dst[1] = v.y; }
     else { dst[0] = v.x; dst[1] = v.y; dst[2] = v.z; dst[3] = v.w; }
@@ -267,7 +286,7 @@ LDEV void vstore(uint8_t* dst, const uint32_t* src) {
     if constexpr (C == 1) v = src[0];
     else if constexpr (C == 2) { v.x = src[0]; v.y = src[1]; }
     else { v.x = src[0]; v.y = src[1]; v.z = src[2]; v.w = src[3]; }
-    *gptr<V>(dst) = v;
+    gst<V>(dst, v);
 }
 
 // One lane's C units of one piece, register layout: for FF8 x[u]; for FF16

@@ -81,16 +81,16 @@ LDEV void ld_unit(uint32_t* x, const uint8_t* piece, uint64_t off) {
         x[1] = x[0] ^ 0x5bd1e995u;
         return;
     }
-    x[0] = *gptr<const uint32_t>(piece + off);
-    x[1] = *gptr<const uint32_t>(piece + off + 32);
+    x[0] = gld<uint32_t>(piece + off);
+    x[1] = gld<uint32_t>(piece + off + 32);
 }
 LDEV void st_unit(uint8_t* piece, uint64_t off, const uint32_t* x) {
     if constexpr ((LAMD_ABLATE & 8) != 0) {  // ablation builds: no piece stores (x kept live)
         if ((x[0] ^ x[1]) == 0x9E3779B9u && off == 0x7FFFFFFFull) *gptr<uint32_t>(piece) = x[0];
         return;
     }
-    *gptr<uint32_t>(piece + off) = x[0];
-    *gptr<uint32_t>(piece + off + 32) = x[1];
+    gst<uint32_t>(piece + off, x[0]);
+    gst<uint32_t>(piece + off + 32, x[1]);
 }
 
 constexpr int lg2(unsigned v) { return v <= 1 ? 0 : 1 + lg2(v >> 1); }

@@ -155,17 +155,21 @@ LDEV Cols strip_cols_lw(uint32_t nunits, unsigned lane) {
 }
 // piece pointer (kernel argument, wave-uniform) + strip base stay scalar: the
 // access is global_load/store with an SGPR base and the lane's VGPR offset.
+#ifndef LAMD_FF8_NT
+#define LAMD_FF8_NT 1  // nontemporal piece I/O in the byte tiles (see gld in rs_device.h)
+#endif
+constexpr bool kFf8Nt = LAMD_FF8_NT != 0;
 LDEV uint32_t gload(uint64_t piece, const Cols& c) {
-    return *gptr<const uint32_t>(reinterpret_cast<const uint8_t*>(piece + c.base) + c.lane_off);
+    return gld<uint32_t, kFf8Nt>(reinterpret_cast<const uint8_t*>(piece + c.base) + c.lane_off);
 }
 LDEV void gstore(uint64_t piece, const Cols& c, uint32_t v) {
-    *gptr<uint32_t>(reinterpret_cast<uint8_t*>(piece + c.base) + c.lane_off) = v;
+    gst<uint32_t, kFf8Nt>(reinterpret_cast<uint8_t*>(piece + c.base) + c.lane_off, v);
 }
 // p: piece pointer with the strip base already added
 LDEV uint32_t gload_at(uint64_t p, const Cols& c) {
-    return *gptr<const uint32_t>(reinterpret_cast<const uint8_t*>(p) + c.lane_off);
+    return gld<uint32_t, kFf8Nt>(reinterpret_cast<const uint8_t*>(p) + c.lane_off);
 }
-LDEV void gstore_at(uint64_t p, const Cols& c, uint32_t v) { *gptr<uint32_t>(reinterpret_cast<uint8_t*>(p) + c.lane_off) = v; }
+LDEV void gstore_at(uint64_t p, const Cols& c, uint32_t v) { gst<uint32_t, kFf8Nt>(reinterpret_cast<uint8_t*>(p) + c.lane_off, v); }
 
 // Strip pointers of the NR consecutive pieces first, first + 1, ... (a lane's
 // registers in layout 0 hold pieces r | w << RB): a slab view steps by its

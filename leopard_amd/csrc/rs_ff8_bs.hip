@@ -337,6 +337,9 @@ LDEV void exchange(Reg& x, uint8_t* area, unsigned g, unsigned l) {
 // -------------------------------------------------------------- kernel -----
 
 // Where one tile (object, 256-byte column strip) lives for this lane.
+#ifndef LAMD_BS_NT
+#define LAMD_BS_NT 3  // nontemporal piece loads (1) and stores (2): +4% on the headline (profiles/r05_v6/nt_ab.txt)
+#endif
 struct BsTile {
     const uint8_t* in;   // piece g << 4 of the strip, + lane offset
     uint8_t* out;
@@ -369,8 +372,13 @@ LDEV void load_half(Reg& x, const BsTile& T) {
         v0.x = uint32_t(uintptr_t(p)) + threadIdx.x, v0.y = v0.x * 3, v0.z = v0.x * 5, v0.w = v0.x * 7;
         v1 = v0 * 11u;
 #else
+#if LAMD_BS_NT & 1
+        const v4u v0 = __builtin_nontemporal_load(gptr<const v4u>(p + T.l0));
+        const v4u v1 = __builtin_nontemporal_load(gptr<const v4u>(p + T.l1));
+#else
         const v4u v0 = *gptr<const v4u>(p + T.l0);
         const v4u v1 = *gptr<const v4u>(p + T.l1);
+#endif
 #endif
         x[r][0] = v0.x, x[r][1] = v0.y, x[r][2] = v0.z, x[r][3] = v0.w;
         x[r][4] = v1.x, x[r][5] = v1.y, x[r][6] = v1.z, x[r][7] = v1.w;
@@ -393,8 +401,13 @@ LDEV void store_half(const Reg& x, const BsTile& T) {
         // strip (always inside: pieces are multiples of 64 bytes), and the
         // transform is column by column, so it holds segment 0's output: it is
         // stored there, the same bytes lane 8 g writes (no branch per store).
+#if LAMD_BS_NT & 2
+        __builtin_nontemporal_store(v0, gptr<v4u>(p + T.l0));
+        __builtin_nontemporal_store(v1, gptr<v4u>(p + T.l1));
+#else
         *gptr<v4u>(p + T.l0) = v0;
         *gptr<v4u>(p + T.l1) = v1;
+#endif
     }
 }
 template <int R0>
@@ -416,6 +429,7 @@ LDEV void transpose_half(Reg& x, const XMasks& xm) {
 // registers while half 1 computes; at the top of the next tile half 1's loads
 // are in flight while half 0 transposes and runs its IFFT layers.
 #ifndef LAMD_BS_STAGGER
+#define LAMD_BS_STAGGER_BLOCKS 0
 #define LAMD_BS_STAGGER 0  // s_sleep 127 (8128 cycles) steps of the second wave of a SIMD (measured: 1, 2, 4 slower)
 #endif
 template <int kForm>
@@ -429,7 +443,11 @@ k_ff8_bs_slab(Ff8SlabBatch b, uint32_t count, uint32_t strips) {
     uint8_t* const area = reinterpret_cast<uint8_t*>(lds + wave * kBsAreaDw);
     unsigned t = blockIdx.x * kBsWaves + wave;
     if (t >= total) return;  // wave-uniform; waves share nothing
+#if LAMD_BS_STAGGER_BLOCKS  // the second half of the grid (the second workgroup of each CU, dispatch order)
+    if (blockIdx.x >= gridDim.x / 2 && t + n < total)
+#else
     if (wave >= kBsWaves / 2 && t + n < total)
+#endif
         for (int i = 0; i < LAMD_BS_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
     const unsigned lane = threadIdx.x & 63u, g = lane >> 3, l = lane & 7u;
     const uint32_t G[3] = {(g & 1u) ? ~0u : 0u, (g & 2u) ? ~0u : 0u, (g & 4u) ? ~0u : 0u};

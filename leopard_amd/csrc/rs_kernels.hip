@@ -76,16 +76,16 @@ LDEV void ld16(uint32_t* x, const uint8_t* base, uint32_t off) {
         x[1] = x[0] ^ 0x5bd1e995u;
         return;
     }
-    x[0] = *gptr<const uint32_t>(base + off);
-    x[1] = *gptr<const uint32_t>(base + off + 32);
+    x[0] = gld<uint32_t>(base + off);
+    x[1] = gld<uint32_t>(base + off + 32);
 }
 LDEV void st16(uint8_t* base, uint32_t off, const uint32_t* x) {
     if constexpr ((LAMD_ABLATE & 8) != 0) {  // experiments: no piece stores (keep x live)
         if ((x[0] ^ x[1]) == 0x9E3779B9u && off == 0x7FFFFFFFu) *gptr<uint32_t>(base) = x[0];
         return;
     }
-    *gptr<uint32_t>(base + off) = x[0];
-    *gptr<uint32_t>(base + off + 32) = x[1];
+    gst<uint32_t>(base + off, x[0]);
+    gst<uint32_t>(base + off + 32, x[1]);
 }
 // piece i of pm when `ok` (wave-uniform), else zeros from the zero page
 LDEV void ld16z(uint32_t* x, const PieceMap& pm, bool ok, unsigned i, const uint8_t* zeros, const Cols16& c) {

@@ -306,6 +306,16 @@ LDEV void ff8_enc(const A& a) {
 #if LAMD_PRIO_LOADS
     __builtin_amdgcn_s_setprio(0);
 #endif
+    // Output piece pointers (pointer-table args): fetched here, behind the
+    // piece loads, as one batch -- fetched at the stores they were eight
+    // dependent scalar-load round trips after the last butterfly (scalar loads
+    // return out of order, so each use waited for every load before it).
+    // Dense: out piece j is ptr[m + j], a compile-time offset, so the batch
+    // merges into one 16-dword scalar load like the input pointers'.
+    uint64_t po[TL::NR];
+    if constexpr (G == 0 && !A::kSlab)
+        fetch_ptrs_by(po, [&](unsigned j) { return kDense ? a.piece(m + j) : a.out_piece(j); },
+                      [&](int r) { return TL::piece(0, r, w); });
     STAMP(1);
     stage.store(tabs);
     __syncthreads();
@@ -341,9 +351,12 @@ LDEV void ff8_enc(const A& a) {
     }
     TL::pin(x);
     uint64_t pp[TL::NR];
-    if constexpr (G == 0)
-        run_ptrs(pp, [&](unsigned j) { return a.out_piece(j); }, TL::piece(0, 0, w), out_stride_of(a), A::kSlab, cl);
-    else {
+    if constexpr (G == 0 && A::kSlab)
+        run_ptrs(pp, [&](unsigned j) { return a.out_piece(j); }, TL::piece(0, 0, w), out_stride_of(a), true, cl);
+    else if constexpr (G == 0) {
+#pragma unroll
+        for (int r = 0; r < TL::NR; ++r) pp[r] = po[r] + cl.base;
+    } else {
 #pragma unroll
         for (int r = 0; r < TL::NR; ++r) pp[r] = a.out_piece(TL::piece(0, r, w)) + cl.base;  // tp < m: R + tp < 256
     }
@@ -500,13 +513,14 @@ LDEV void ff8_dec(const Ff8DecArgs& a) {
     ElRegs<TL::NR> el;
     el.load(a, pos(0));
     typename TL::Reg v;
-    {
-        // received pieces: positions [0, R) recovery, [m, m + K) originals (LeopardFF8.cpp:1857-1877)
-        uint64_t pp[TL::NR];
-        fetch_ptrs(pp, a, pos);
+    // received pieces: positions [0, R) recovery, [m, m + K) originals
+    // (LeopardFF8.cpp:1857-1877); a lost original's position holds its output
+    // buffer, so these pointers also serve the stores (kept in SGPRs: a second
+    // fetch after the butterflies was a scalar-load round trip in front of them)
+    uint64_t pp[TL::NR];
+    fetch_ptrs(pp, a, pos);
 #pragma unroll
-        for (int r = 0; r < TL::NR; ++r) v[r][0] = present(pos(r), 0) ? gload(pp[r], cl) : 0u;
-    }
+    for (int r = 0; r < TL::NR; ++r) v[r][0] = present(pos(r), 0) ? gload(pp[r], cl) : 0u;
     STAMP(1);
     sk_stage.store(sk);
     log_stage.store(ltab);
@@ -534,8 +548,6 @@ LDEV void ff8_dec(const Ff8DecArgs& a) {
     STAMP(5);
     TL::pin(v);
     // lost original at p = m + i: work[i] = z[p] * exp(-el[p])  (LeopardFF8.cpp:1913-1915)
-    uint64_t pp[TL::NR];
-    fetch_ptrs(pp, a, pos);
     auto is_needed = [&](int r) { return needed(pos(r), 0); };
     scale_batched<TL>(v, ltab, [&](int r) { return F::kModulus - el.at(r); }, is_needed);
     if (!cl.live) return;
@@ -599,6 +611,9 @@ LDEV void ff8_dec_half(const Ff8DecArgs& a) {
 #pragma unroll
         for (int r = 0; r < TL::NR; ++r) v[r][0] = present(lpos(r), 0) ? gload(pp[r], cl) : 0u;
     }
+    // output pointers now, behind the piece loads (not after the butterflies)
+    uint64_t pp[TL::NR];
+    fetch_ptrs(pp, a, hpos);
     sk_stage.store(sk);
     log_stage.store(ltab);
     __syncthreads();
@@ -611,8 +626,6 @@ LDEV void ff8_dec_half(const Ff8DecArgs& a) {
     TL::fused_top(v, FF8::tab_at(a.fused));
     TL::template fft<true>(v, w, lane, lds, high, win, needed);
     TL::pin(v);
-    uint64_t pp[TL::NR];
-    fetch_ptrs(pp, a, hpos);
     auto is_needed = [&](int r) { return needed(hpos(r), 0); };
     scale_batched<TL>(v, ltab, [&](int r) { return F::kModulus - el_hi.at(r); }, is_needed);
     if (!cl.live) return;
@@ -663,11 +676,13 @@ LDEV void ff8_dec_split(const Ff8DecArgs& a) {
     el_lo.load(a, lpos(0));
     el_hi.load(a, hpos(0));
     typename TL::Reg x, h;
+    // high positions: surviving originals in, lost originals out (kept for the stores)
+    uint64_t ph[TL::NR];
+    fetch_ptrs(ph, a, hpos);
+#pragma unroll
+    for (int r = 0; r < TL::NR; ++r) h[r][0] = present(hpos(r), 0) ? gload(ph[r], cl) : 0u;
     {
         uint64_t pp[TL::NR];
-        fetch_ptrs(pp, a, hpos);
-#pragma unroll
-        for (int r = 0; r < TL::NR; ++r) h[r][0] = present(hpos(r), 0) ? gload(pp[r], cl) : 0u;
         fetch_ptrs(pp, a, lpos);
 #pragma unroll
         for (int r = 0; r < TL::NR; ++r) x[r][0] = present(lpos(r), 0) ? gload(pp[r], cl) : 0u;
@@ -689,14 +704,12 @@ LDEV void ff8_dec_split(const Ff8DecArgs& a) {
     TL::xor_into(x, y);
     TL::template fft<false>(x, w, lane, lds, high, win, needed);
     TL::pin(x);
-    uint64_t pp[TL::NR];
-    fetch_ptrs(pp, a, hpos);
     auto is_needed = [&](int r) { return needed(hpos(r), 0); };
     scale_batched<TL>(x, ltab, [&](int r) { return F::kModulus - el_hi.at(r); }, is_needed);
     if (!cl.live) return;
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r)
-        if (is_needed(r)) gstore(pp[r], cl, x[r][0]);
+        if (is_needed(r)) gstore(ph[r], cl, x[r][0]);
 }
 template <int T, int RB>
 __global__ void __launch_bounds__(threads_for(T, RB), 4) k_ff8_dec_split(Ff8DecArgs a) {

@@ -406,6 +406,9 @@ struct Pyr16Live {
 // absent.  Positions: [0, m) recovery (only [0, R) exist), [m, m+K) originals
 // (LeopardFF8.cpp:1857-1877).  Branch-free on the vector side: an absent piece
 // reads the zero page at unit 0.
+#ifndef LAMD_DEC_LO_RUN
+#define LAMD_DEC_LO_RUN 1
+#endif
 LDEV void load_received(uint32_t* x, const DecArgs& a, unsigned p, const Cols16& c) {
     const uint8_t* base = a.zeros;
     if (!bit_set(a.erased_dev, p)) {
@@ -413,6 +416,32 @@ LDEV void load_received(uint32_t* x, const DecArgs& a, unsigned p, const Cols16&
         else if (p >= a.m && p < a.m + a.K) base = a.orig.ptr(p - a.m) + c.strip;
     }
     ld16(x, base, c.off);
+}
+
+// The NR received pieces at positions p0 .. p0 + NR - 1 (a lane's registers
+// in layout 0; p0 a multiple of NR <= 32): the erasure bits come from one
+// word and every piece pointer is fetched before the first piece load issues.
+// (load_received per piece chained an erasure-word scalar load, a wait, a
+// branch, a pointer scalar load and a wait in front of each piece load.)
+template <int NR, class Reg>
+LDEV void load_received_run(Reg& v, const DecArgs& a, unsigned p0, const Cols16& c) {
+    static_assert(NR <= 32 && (NR & (NR - 1)) == 0, "positions inside one erasure word");
+    const uint32_t ew = cload(a.erased_dev + (p0 >> 5)) >> (p0 & 31);
+    const uint8_t* base[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const unsigned p = p0 + unsigned(r);
+        const uint8_t* b = a.zeros;
+        if (!((ew >> r) & 1u)) {
+            if (p < a.R) b = a.rec.ptr(p) + c.strip;
+            else if (p >= a.m && p < a.m + a.K) b = a.orig.ptr(p - a.m) + c.strip;
+        }
+        base[r] = b;
+    }
+#pragma unroll
+    for (int r = 0; r < NR; ++r) asm volatile("" : "+s"(base[r]));
+#pragma unroll
+    for (int r = 0; r < NR; ++r) ld16(v[r], base[r], c.off);
 }
 
 // pass 1: scale-on-load + IFFT over the low bits -> a_out[g].  LDS: exchange
@@ -436,8 +465,13 @@ __global__ void __launch_bounds__(threads16(kLoBits, R), 4) k_dec_lo(DecArgs a) 
     LogTabs16Stage<NT, (1u << T)> ls;
     ls.load(a.tabs, a.scale_logs + (y << T));
     typename TL::Reg v;
+    static_assert(TL::lo(0) == 0, "layout 0: register r holds position r | w << R");
+#if LAMD_DEC_LO_RUN
+    load_received_run<TL::NR>(v, a, ps.global(TL::piece(0, 0, w)), cl);
+#else
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) load_received(v[r], a, ps.global(TL::piece(0, r, w)), cl);
+#endif
     st.store(set);
     ls.store(scl);
     __syncthreads();
@@ -558,6 +592,21 @@ __global__ void __launch_bounds__(threads16(kLoBits, R), 4) k_dec_fin(DecArgs a)
     typename TL::Reg z;
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) ld16(z[r], a.a_in.slab_ptr(ps.global(TL::piece(TL::kLast, r, w))) + cl.strip, cl.off);
+    // output pointers of the lane's lost originals (layout 0: positions p0 + r),
+    // fetched here as one batch behind the slab loads: at the stores each was an
+    // erasure-word and a pointer scalar load, waited for one after the other
+    static_assert(TL::lo(0) == 0, "layout 0: register r holds position r | w << R");
+    const unsigned p0 = ps.global(TL::piece(0, 0, w));
+    const uint32_t ew = cload(a.erased_dev + (p0 >> 5)) >> (p0 & 31);
+    uint8_t* op[TL::NR];
+#pragma unroll
+    for (int r = 0; r < TL::NR; ++r) {
+        const unsigned p = p0 + unsigned(r);
+        op[r] = nullptr;
+        if (p >= a.m && p < a.m + a.K && ((ew >> r) & 1u)) op[r] = a.out.ptr(p - a.m) + cl.strip;
+    }
+#pragma unroll
+    for (int r = 0; r < TL::NR; ++r) asm volatile("" : "+s"(op[r]));
     st.store(set);
     ls.store(rvl);
     __syncthreads();
@@ -570,14 +619,13 @@ __global__ void __launch_bounds__(threads16(kLoBits, R), 4) k_dec_fin(DecArgs a)
     if (!live) return;
 #pragma unroll
     for (int r = 0; r < TL::NR; ++r) {
-        const unsigned p = ps.global(TL::piece(0, r, w));
-        if (p >= a.m && p < a.m + a.K && bit_set(a.erased_dev, p)) {
+        if (op[r] != nullptr) {
             uint32_t o[2 * C];
             asm volatile("" ::: "memory");
             const FF16::Tab t = FF16::tab_lds(rvl + tab16_slot(TL::piece(0, r, w)));
 #pragma unroll
             for (int u = 0; u < C; ++u) FF16::mul(&o[u * 2], &z[r][u * 2], t);
-            st16(a.out.ptr(p - a.m) + cl.strip, cl.off, o);
+            st16(op[r], cl.off, o);
         }
         __builtin_amdgcn_sched_barrier(0);
     }

@@ -8,9 +8,11 @@
 #define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
 
 struct Small { unsigned long long p; };
-struct Big { unsigned long long p[500]; };  // ~4 KB, like Ff8EncArgs
+struct Big { unsigned long long p[500]; };  // ~4 KB
+struct Mid { unsigned long long p[270]; };  // ~2.1 KB, like Ff8EncArgs
 
 __global__ void k_small(Small a) { if (a.p == 1234567) ((int*)a.p)[threadIdx.x] = 0; }
+__global__ void k_mid(Mid a) { if (a.p[0] == 1234567) ((int*)a.p[0])[threadIdx.x] = 0; }
 __global__ void k_big(Big a) { if (a.p[0] == 1234567) ((int*)a.p[0])[threadIdx.x] = 0; }
 __global__ void k_lds(Small a) {
     extern __shared__ int lds[];
@@ -29,6 +31,7 @@ int main() {
     CHECK(hipEventCreate(&b));
     Small sm{0};
     Big bg{};
+    Mid md{};
     CHECK(hipFuncSetAttribute((const void*)k_lds, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     auto run = [&](const char* name, auto launch) {
         for (int i = 0; i < 10; ++i) launch();
@@ -45,6 +48,7 @@ int main() {
         return 0;
     };
     run("empty 256 x 1024, 8 B args", [&] { hipLaunchKernelGGL(k_small, dim3(256), dim3(1024), 0, s, sm); });
+    run("empty 256 x 1024, 2.1 KB args", [&] { hipLaunchKernelGGL(k_mid, dim3(256), dim3(1024), 0, s, md); });
     run("empty 256 x 1024, 4 KB args", [&] { hipLaunchKernelGGL(k_big, dim3(256), dim3(1024), 0, s, bg); });
     run("empty 256 x 512, 4 KB args", [&] { hipLaunchKernelGGL(k_big, dim3(256), dim3(512), 0, s, bg); });
     run("empty 256 x 256, 8 B args", [&] { hipLaunchKernelGGL(k_small, dim3(256), dim3(256), 0, s, sm); });

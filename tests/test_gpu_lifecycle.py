@@ -405,3 +405,26 @@ def test_tuning_switches_at_non_default_values():
     code = _TUNED_SCRIPT.format(repo=os.path.dirname(here), tests=here)
     p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110)
     assert p.returncode == 0 and "tuned ok" in p.stdout, (p.stdout[-2000:], p.stderr[-3000:])
+
+
+@pytest.mark.gpu
+def test_bench_line_batch_timing_small():
+    """bench.py end to end at a small size (4 objects in launches of 2, 2 streams):
+    one JSON line whose roofline launch time comes from the events inside the
+    timed region (GPU time per launch <= a launch's own span; achieved =
+    algorithmic bytes / launch time)."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--steps", "3", "--warmup", "1",
+                        "--objects", "4", "--launch-objects", "2", "--sets", "8", "--no-host", "--no-cpu-baseline",
+                        "--no-sharded", "--no-secondary"], capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = json.loads(p.stdout.strip().splitlines()[-1])
+    r = d["roofline"]
+    assert d["value"] > 0 and d["config"]["mode"] == "batch" and d["config"]["objects_per_launch"] == 2
+    span = max(r["launch_span_encode_us"], r["launch_span_decode_us"])
+    assert 0 < r["launch_us"] <= span * 1.05
+    assert abs(r["achieved"] - r["algorithmic_bytes_per_launch"] / r["launch_us"] / 1e3) <= 0.01 * r["achieved"] + 0.01
+    assert r["frac"] < 1.0

@@ -337,6 +337,9 @@ LDEV void exchange(Reg& x, uint8_t* area, unsigned g, unsigned l) {
 // -------------------------------------------------------------- kernel -----
 
 // Where one tile (object, 256-byte column strip) lives for this lane.
+#ifndef LAMD_BS_PRIO
+#define LAMD_BS_PRIO 0
+#endif
 #ifndef LAMD_BS_NT
 #define LAMD_BS_NT 3  // nontemporal piece loads (1) and stores (2): +4% on the headline (profiles/r05_v6/nt_ab.txt)
 #endif
@@ -486,7 +489,13 @@ k_ff8_bs_slab(Ff8SlabBatch b, uint32_t count, uint32_t strips) {
         transpose_half<0>(x, xm);
 #endif
         store_half<0>(x, cur);
+#if LAMD_BS_PRIO
+        __builtin_amdgcn_s_setprio(LAMD_BS_PRIO);  // experiments: issue the next tile's loads ahead of the other wave's arithmetic
+#endif
         if (more) load_half<0>(x, nxt);
+#if LAMD_BS_PRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
 #ifndef ABL_ARITH
         layer_low<false, kOffF, 2, 8>(x, G);
         layer_low<false, kOffF, 1, 8>(x, G);
@@ -495,7 +504,13 @@ k_ff8_bs_slab(Ff8SlabBatch b, uint32_t count, uint32_t strips) {
 #endif
         store_half<8>(x, cur);
         if (!more) break;
+#if LAMD_BS_PRIO
+        __builtin_amdgcn_s_setprio(LAMD_BS_PRIO);
+#endif
         load_half<8>(x, nxt);
+#if LAMD_BS_PRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
         t = tn;
         cur = nxt;
     }

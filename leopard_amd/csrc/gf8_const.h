@@ -7,7 +7,8 @@
 // the library uses): logs via the LFSR of polynomial 0x11D over the Cantor
 // basis (LeopardFF8.cpp:46-48, 158-194), FFT skews by FFTInitialize
 // (LeopardFF8.cpp:496-531).  tests/test_cpu_gf8_const.py checks these tables
-// against the host library's.
+// and every multiply matrix against the host library's tables, the oracle's and
+// the reference's own LogLUT / ExpLUT / FFTSkew (compiled reference, oracle/_ref).
 #pragma once
 
 #include <cstdint>

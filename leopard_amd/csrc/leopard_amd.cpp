@@ -288,6 +288,22 @@ struct Workspace {
             return size_t(h);
         }
     };
+    // Tile queues of the bit-sliced batch kernel (rs_ff8_bs.hip): two sets of
+    // kBsQueueDw counters; launch i on this stream takes set i & 1 and zeroes
+    // the other one, which launch i - 1 used and has finished with (stream order).
+    uint32_t* bsq = nullptr;
+    unsigned bsq_launches = 0;
+    LeopardResult bs_queue(uint32_t** use, uint32_t** clear) {
+        touched = true;
+        if (!bsq) {
+            HIP_OK(pool_alloc(reinterpret_cast<void**>(&bsq), 2 * kBsQueueDw * 4, dev, stream), "allocate tile queues");
+            HIP_OK(hipMemsetAsync(bsq, 0, 2 * kBsQueueDw * 4, stream), "clear tile queues");
+        }
+        *use = bsq + (bsq_launches & 1u) * kBsQueueDw;
+        *clear = bsq + ((bsq_launches + 1) & 1u) * kBsQueueDw;
+        ++bsq_launches;
+        return Leopard_Success;
+    }
     static constexpr unsigned kEl8Slots = 512;
     uint32_t* el8 = nullptr;
     std::unordered_map<El8Key, unsigned, El8Hash> el8_map;
@@ -324,7 +340,7 @@ struct Workspace {
             if (sl.done) (void)hipEventDestroy(sl.done);
             sl = StageSlot{};
         }
-        release_device_memory(dev, {dbuf, ring_dev, direct, el8});
+        release_device_memory(dev, {dbuf, ring_dev, direct, el8, bsq});
         if (el8_host) (void)hipHostFree(el8_host);
         el8_host = nullptr;
         for (int e = 0; e < kEl8Events; ++e) {
@@ -340,6 +356,8 @@ struct Workspace {
             d = Dec16Slot{};
         }
         el8 = nullptr;
+        bsq = nullptr;
+        bsq_launches = 0;
         el8_map.clear();
         el8_key.clear();
         el8_stamp.clear();
@@ -2089,7 +2107,11 @@ bool run_slab_batch8(int dev, RangeCache& rc, unsigned count, uint64_t bytes, un
                 b.out_base[j] = ob[o0 + j];
                 b.out_stride[j] = os[o0 + j];
             }
-            HIP_OK(launch_ff8_encode_slab(T, b, n, multi, form, c.s), "slab batch kernel");
+            uint32_t *q = nullptr, *qclear = nullptr;
+            if (form != kFormGeneral && !multi && ff8_bs_supported(T, K, R, b.nchunks) &&
+                (r = c.ws->bs_queue(&q, &qclear)) != Leopard_Success)
+                return r;
+            HIP_OK(launch_ff8_encode_slab(T, b, n, multi, form, c.s, q, qclear), "slab batch kernel");
         }
         return finish(c, false);
     }();

@@ -662,7 +662,7 @@ def test_bitsliced_dense_tile_matches_oracle(leo, b):
                                    [[w[i].data_ptr() for i in range(wc)] for w in works])
     assert res == leo.LeopardResult.Success, leo.last_error()
     torch.cuda.synchronize()
-    for o in ([0, 1, count - 1] if count > 3 else range(count)):
+    for o in range(count):  # every object of every launch
         assert np.array_equal(works[o][:r].cpu().numpy(), ol.oracle().encode(objs[o], r)), o
     dworks = [torch.zeros((dwc, b), dtype=torch.uint8, device="cuda") for _ in range(count)]
     res = leo.leo_amd_decode_batch(b, k, r, dwc, [[None] * k] * count,
@@ -672,6 +672,35 @@ def test_bitsliced_dense_tile_matches_oracle(leo, b):
     torch.cuda.synchronize()
     for o in range(count):
         assert torch.equal(dworks[o][:k], dev[o]), o
+
+
+def test_bitsliced_headline_geometry(leo):
+    """The benchmark's own launch: ONE encode-batch and ONE decode-batch launch
+    over 64 objects of 128 + 128 x 65536 B laid out as slabs (bench.py
+    `headline`, BASELINE configs[1]).  Four objects spread over the launch
+    (first, two inside, last: different waves, rounds of the persistent grid
+    and prefetch slots) are checked against the oracle; the full-loss decode
+    of every object must give back its originals."""
+    k = r = 128
+    b, count = 65536, 64
+    gen = torch.Generator(device="cuda").manual_seed(128)
+    data = torch.randint(0, 256, (count, k, b), dtype=torch.uint8, device="cuda", generator=gen)
+    wc, dwc = leo.leo_encode_work_count(k, r), leo.leo_decode_work_count(k, r)
+    works = torch.zeros((count, wc, b), dtype=torch.uint8, device="cuda")
+    res = leo.leo_amd_encode_batch(b, k, r, wc, [[data[o, i].data_ptr() for i in range(k)] for o in range(count)],
+                                   [[works[o, i].data_ptr() for i in range(wc)] for o in range(count)])
+    assert res == leo.LeopardResult.Success, leo.last_error()
+    torch.cuda.synchronize()
+    for o in (0, 21, 42, count - 1):
+        assert np.array_equal(works[o, :r].cpu().numpy(), ol.oracle().encode(data[o].cpu().numpy(), r)), o
+    dworks = torch.zeros((count, dwc, b), dtype=torch.uint8, device="cuda")
+    res = leo.leo_amd_decode_batch(b, k, r, dwc, [[None] * k] * count,
+                                   [[works[o, i].data_ptr() for i in range(r)] for o in range(count)],
+                                   [[dworks[o, i].data_ptr() for i in range(dwc)] for o in range(count)])
+    assert res == leo.LeopardResult.Success, leo.last_error()
+    torch.cuda.synchronize()
+    for o in range(count):
+        assert torch.equal(dworks[o, :k], data[o]), o
 
 
 def test_decoder_pattern_caches_evict_and_refill(leo):

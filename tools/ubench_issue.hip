@@ -1,7 +1,8 @@
 // Microbenchmark (performance experiment only): VALU issue cost on gfx950 at
 // 1, 2, 3 and 4 waves per SIMD for the instruction forms of the bit-sliced
 // GF(2^8) tile (rs_ff8_bs.hip): v_xor_b32 (VOP2), v_bitop3_b32 with three
-// VGPR sources, v_bitop3_b32 with an SGPR source, each in C independent chains.
+// VGPR sources, v_bitop3_b32 with an SGPR source, each in C independent chains;
+// and the lane exchanges (v_permlane16/32_swap, DPP row_ror:8 forms).
 // Reports SIMD cycles per instruction (wall time x clock / instructions per
 // SIMD) and per-wave cycles per instruction (s_memtime inside the kernel).
 //   hipcc --offload-arch=gfx950 -O3 -o tools/bin/ubench_issue tools/ubench_issue.hip
@@ -39,6 +40,12 @@ __global__ void __launch_bounds__(256) k_issue(uint32_t* out, uint64_t* clk, uin
                 if constexpr (OP == 1) asm volatile("v_bitop3_b32 %0, %1, %2, %0 bitop3:0x96" : "+v"(v[i]) : "v"(w[i]), "v"(w[(i + 1) % C]));
                 if constexpr (OP == 2) asm volatile("v_bitop3_b32 %0, %1, %2, %0 bitop3:0x78" : "+v"(v[i]) : "v"(w[i]), "s"(s));
                 if constexpr (OP == 3) asm volatile("v_lshlrev_b32 %0, 1, %0" : "+v"(v[i]));
+                // lane exchanges (chains >= 4: no DPP / permlane read-after-write hazard inside a chain)
+                if constexpr (OP == 4) asm volatile("v_permlane32_swap_b32 %0, %1" : "+v"(v[i]), "+v"(w[i]));
+                if constexpr (OP == 5) asm volatile("v_permlane16_swap_b32 %0, %1" : "+v"(v[i]), "+v"(w[i]));
+                if constexpr (OP == 6) asm volatile("v_cndmask_b32_dpp %0, %1, %0, vcc row_ror:8 row_mask:0xf bank_mask:0xf" : "+v"(v[i]) : "v"(w[i]));
+                if constexpr (OP == 7) asm volatile("v_mov_b32_dpp %0, %1 row_ror:8 row_mask:0xf bank_mask:0xf" : "=v"(v[i]) : "v"(w[(i + 1) % C]));
+                if constexpr (OP == 8) asm volatile("v_xor_b32_dpp %0, %1, %0 row_ror:8 row_mask:0xf bank_mask:0xf" : "+v"(v[i]) : "v"(w[i]));
             }
     }
     const uint64_t t1 = __builtin_amdgcn_s_memtime();
@@ -86,5 +93,10 @@ int main() {
     R("v_bitop3_b32 (3 VGPR)", 1, 1) R("v_bitop3_b32 (3 VGPR)", 1, 2) R("v_bitop3_b32 (3 VGPR)", 1, 4) R("v_bitop3_b32 (3 VGPR)", 1, 8)
     R("v_bitop3_b32 (2 VGPR + SGPR)", 2, 1) R("v_bitop3_b32 (2 VGPR + SGPR)", 2, 4) R("v_bitop3_b32 (2 VGPR + SGPR)", 2, 8)
     R("v_lshlrev_b32", 3, 1) R("v_lshlrev_b32", 3, 4) R("v_lshlrev_b32", 3, 8)
+    R("v_permlane32_swap_b32", 4, 4) R("v_permlane32_swap_b32", 4, 8)
+    R("v_permlane16_swap_b32", 5, 4) R("v_permlane16_swap_b32", 5, 8)
+    R("v_cndmask_b32_dpp row_ror:8", 6, 4) R("v_cndmask_b32_dpp row_ror:8", 6, 8)
+    R("v_mov_b32_dpp row_ror:8", 7, 4) R("v_mov_b32_dpp row_ror:8", 7, 8)
+    R("v_xor_b32_dpp row_ror:8", 8, 4) R("v_xor_b32_dpp row_ror:8", 8, 8)
     return 0;
 }

@@ -26,7 +26,8 @@ max-over-ranks time.
 
 configs[4] (`sharded_object`): ONE 32768+32768 x 64 KiB object (2 GiB of
 originals, GF(2^16)) column-sharded over the N ranks -- rank g runs
-leo_amd_encode_slice / leo_amd_decode_slice on its B/N columns of every piece
+leo_amd_encode_slice / leo_amd_decode_slice on its B/N columns of every piece,
+which it alone allocates (pieces of B/N bytes holding those columns' bytes)
 -- timed with a barrier and max over ranks ("strong" scaling: the object is
 fixed as N grows).  With N > 1, rank 0 also times the whole object alone on
 its GPU in the same run, so the line carries the 1-GPU time of that object.
@@ -165,9 +166,11 @@ def stub_rank(world, rank):
         print(json.dumps({"stub": True, "world": world, "max_over_ranks": el, "ranks": ranks}), flush=True)
 
 
-def hash_fill_cuda(torch, seed, pieces, nbytes, device):
+def hash_fill_cuda(torch, seed, pieces, nbytes, device, full_bytes=None, col0=0):
     """Synthetic piece bytes on the device: a 32-bit counter hash of the global
-    byte index (same bytes as tests/oracle_lib.hash_bytes)."""
+    byte index (same bytes as tests/oracle_lib.hash_bytes).  With full_bytes:
+    columns [col0, col0 + nbytes) of pieces of full_bytes bytes (a column
+    shard holds the same bytes as those columns of the whole object)."""
     out = torch.empty((pieces, nbytes), dtype=torch.uint8, device=device)
     flat = out.view(-1)
     step = 1 << 26
@@ -175,6 +178,8 @@ def hash_fill_cuda(torch, seed, pieces, nbytes, device):
     for s in range(0, flat.numel(), step):
         e = min(flat.numel(), s + step)
         g = torch.arange(s, e, dtype=torch.int64, device=device)
+        if full_bytes is not None:
+            g = (g // nbytes) * full_bytes + col0 + g % nbytes
         x = (g * 2654435761 + seed * 0x632BE5AB) & M
         x = x ^ (x >> 16)
         x = (x * 0x85EBCA6B) & M
@@ -279,11 +284,13 @@ def main():
     if rank == 0:
         k, r, nbytes = args.K, args.R, args.bytes
         batch = args.mode == "batch"
-        traffic = pmc_traffic(head["dominant"][0], k, r, nbytes, head["launch_objects"] if batch else 1)
+        kern1 = kernels_for(k, r, nbytes, k)
+        traffic = pmc_traffic(head["dominant"][0], k, r, nbytes, head["launch_objects"] if batch else 1,
+                              kernels="k_ff8_bs_slab" if batch else kern1[head["dominant"][0]], loss=k)
         kind, algo, t_kernel = head["dominant"]
         achieved = algo / t_kernel / 1e9
         s_kind, s_algo, s_t = head["single_dominant"]
-        s_traffic = pmc_traffic(s_kind, k, r, nbytes, 1)
+        s_traffic = pmc_traffic(s_kind, k, r, nbytes, 1, kernels=kern1[s_kind], loss=k)
         kname = ("k_ff8_bs_slab<1> / <2>: %d-object encode-batch / decode-batch launches (bit-sliced tile; "
                  "dense encode form / full-loss decode form)" % head["launch_objects"]) if batch else kind
         out = {
@@ -341,6 +348,12 @@ def main():
                                          "pre->post event interval, the rocprofv3 kernel-trace duration, which "
                                          "counts the time it overlaps the neighbouring launch on the other "
                                          "stream" if batch else "back-to-back single calls behind a spin kernel"),
+                         # busy is this rank's wall GPU time per launch: where ranks share a device the
+                         # other ranks' launches run inside it, so the fraction is not the kernel's own
+                         **({"shared_device": True,
+                             "shared_device_note": "ranks share a device: launch_us holds the other ranks' "
+                                                   "launches too; achieved / frac understate the kernel"}
+                            if n_devices < world else {}),
                          **({"launch_span_encode_us": round(head["span_enc"] * 1e6, 3),
                              "launch_span_decode_us": round(head["span_dec"] * 1e6, 3)} if batch else {}),
                          # per-config fractions as scalars (the driver's record keeps scalars only)
@@ -575,52 +588,62 @@ def configs4_sharded(args, leo, torch, device, barrier, rank, world, max_over_ra
     """BASELINE configs[4]: one 32768+32768 x 64 KiB object, column-sharded over
     the ranks (leopard_amd.sharding -> leo_amd_encode_slice / decode_slice; the
     codec being sharded is LeopardFF16.cpp:1397-1467, 1652-1775).  Each rank
-    holds every piece at full size and touches only its columns."""
+    allocates only its own column shard of every piece (its columns of the
+    object's bytes, as B/N-byte pieces: memory and placement as in a real
+    N-way split) and codes it with the slice calls at offset 0."""
     from leopard_amd.sharding import shard_for_rank
     lib = leo.lib
     k = r = 32768
     b = 65536
     wc, dwc = leo.leo_encode_work_count(k, r), leo.leo_decode_work_count(k, r)
-    data = hash_fill_cuda(torch, 7, k, b, device)
-    work = torch.empty((wc, b), dtype=torch.uint8, device=device)
-    dwork = torch.empty((dwc, b), dtype=torch.uint8, device=device)
-    po, pw, pr, pd = ptrs(data), ptrs(work), ptrs(work, r), ptrs(dwork)
-    pn = (VP * k)()  # every original lost
+    off, size = shard_for_rank(b, rank, world)
     stream = torch.cuda.current_stream(device)
     leo.set_stream(stream.cuda_stream)
 
-    def step(off, size):
-        if lib.leo_amd_encode_slice(b, off, size, k, r, wc, po, pw) != 0:
+    def shard(width, col0):  # pieces of `width` bytes = columns [col0, col0 + width) of the object
+        data = hash_fill_cuda(torch, 7, k, width, device, full_bytes=b, col0=col0)
+        work = torch.empty((wc, width), dtype=torch.uint8, device=device)
+        dwork = torch.empty((dwc, width), dtype=torch.uint8, device=device)
+        return data, work, dwork, (ptrs(data), ptrs(work), ptrs(work, r), ptrs(dwork))
+
+    pn = (VP * k)()  # every original lost
+
+    def step(width, p):
+        po, pw, pr, pd = p
+        if lib.leo_amd_encode_slice(width, 0, width, k, r, wc, po, pw) != 0:
             raise RuntimeError(leo.last_error())
-        if lib.leo_amd_decode_slice(b, off, size, k, r, dwc, pn, pr, pd) != 0:
+        if lib.leo_amd_decode_slice(width, 0, width, k, r, dwc, pn, pr, pd) != 0:
             raise RuntimeError(leo.last_error())
 
-    off, size = shard_for_rank(b, rank, world)
-    step(off, size)
+    data, work, dwork, pp = shard(size, off)
+    step(size, pp)
     torch.cuda.synchronize()
-    ok = bool(torch.equal(dwork[:k, off:off + size], data[:, off:off + size]))
+    ok = bool(torch.equal(dwork[:k], data))
     if world > 1:  # every rank's columns round-trip
         ok = max_over_ranks(0.0 if ok else 1.0) == 0.0
     nsteps = args.sharded_steps or max(1, min(args.steps, 10))
-    step(off, size)
+    step(size, pp)
     barrier()
     t0 = time.perf_counter()
     for _ in range(nsteps):
-        step(off, size)
+        step(size, pp)
     torch.cuda.synchronize()
     el_local = time.perf_counter() - t0
     el = max_over_ranks(el_local)
     n1_ms = None
-    if world > 1:  # the same object on one GPU (rank 0 alone) for the strong-scaling ratio
+    if world > 1:  # the same object on one GPU (rank 0 alone, whole pieces) for the strong-scaling ratio
         barrier()
         if rank == 0:
-            step(0, b)
+            full = shard(b, 0)
+            step(b, full[3])
             torch.cuda.synchronize()
             a = time.perf_counter()
             for _ in range(max(1, nsteps // 2)):
-                step(0, b)
+                step(b, full[3])
             torch.cuda.synchronize()
             n1_ms = (time.perf_counter() - a) / max(1, nsteps // 2) * 1e3
+            del full
+            torch.cuda.empty_cache()
         barrier()
     ms = el / nsteps * 1e3
     ndev = n_devices or world  # distinct GPUs under the ranks (ranks may share one)
@@ -628,7 +651,8 @@ def configs4_sharded(args, leo, torch, device, barrier, rank, world, max_over_ra
     res = {"workload": f"configs[4]: one {k}+{r} x {b} B object (GF(2^16), encode + full-loss decode), "
                        f"column-sharded over {world} rank(s) on {ndev} GPU(s): "
                        f"{b // world if b % world == 0 else size} B of every "
-                       f"piece per rank via leo_amd_encode_slice / leo_amd_decode_slice",
+                       f"piece per rank, allocated per rank as pieces of that width (its columns of the "
+                       f"object's bytes), via leo_amd_encode_slice / leo_amd_decode_slice",
            "value": round(k * b * nsteps / el / 1e9, 3), "unit": "GB/s", "scaling": "strong",
            "n_gpus": ndev, "world": world, "ms_per_step": round(ms, 3), "steps": nsteps, "roundtrip_ok": ok,
            "roofline": {"bound": "hbm", "achieved_per_gpu": round(algo / ndev / (ms / 1e3) / 1e9, 2),
@@ -647,12 +671,14 @@ def configs4_sharded(args, leo, torch, device, barrier, rank, world, max_over_ra
         e1.synchronize()
         return e0.elapsed_time(e1) / reps
 
+    po, pw, pr, pd = pp
+
     def enc():
-        if lib.leo_amd_encode_slice(b, off, size, k, r, wc, po, pw) != 0:
+        if lib.leo_amd_encode_slice(size, 0, size, k, r, wc, po, pw) != 0:
             raise RuntimeError(leo.last_error())
 
     def dec():
-        if lib.leo_amd_decode_slice(b, off, size, k, r, dwc, pn, pr, pd) != 0:
+        if lib.leo_amd_decode_slice(size, 0, size, k, r, dwc, pn, pr, pd) != 0:
             raise RuntimeError(leo.last_error())
 
     kern = kernels_for(k, r, size, k)
@@ -660,7 +686,7 @@ def configs4_sharded(args, leo, torch, device, barrier, rank, world, max_over_ra
     for kind, fn in (("encode", enc), ("decode", dec)):
         cms = timed(fn)
         algo1 = (k + r) * size
-        t = pmc_traffic(kind, k, r, b) if size == b else {}
+        t = pmc_traffic(kind, k, r, b, kernels=kern[kind], loss=k) if size == b else {}
         per[kind] = {"ms": round(cms, 3), "kernel": kern[kind], "achieved": round(algo1 / cms / 1e6, 2),
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(algo1 / cms / 1e6 / HBM_PEAK_GBPS, 4),
                      "algorithmic_bytes": algo1, "traffic": t.get("bytes"), "traffic_source": t.get("source")}
@@ -752,7 +778,7 @@ def run_shape(leo, torch, device, k, r, nbytes, loss, n=3):
     kern = kernels_for(k, r, nbytes, loss)
 
     def roof(kind, us, algo):  # roofline of the call's kernels, PMC traffic when committed for this shape
-        t = pmc_traffic(kind, k, r, nbytes)
+        t = pmc_traffic(kind, k, r, nbytes, kernels=kern[kind], loss=loss)
         return {"bound": "hbm", "kernel": kern.get(kind) if isinstance(kern, dict) else None,
                 "achieved": round(algo / us / 1e3, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(algo / us / 1e3 / HBM_PEAK_GBPS, 4), "algorithmic_bytes": algo,
@@ -895,12 +921,25 @@ def _profile_order(path):
     return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
 
 
-def pmc_traffic(kernel, k, r, nbytes, objects=1):
-    """HBM bytes per launch of the dominant kernel from the newest committed PMC
-    pass (tools/pmc_traffic.py: FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md
-    HBM section; profiles/rNN_vMM ordered by round, then version), when one
-    exists for this workload; else None."""
+def kernel_bases(names):
+    """The kernel base names (template arguments dropped) in a '+'-joined list,
+    without the ones a call launches only for a new erasure pattern."""
+    import re
+    return frozenset(m.group(1) for m in re.finditer(r"(k_[A-Za-z0-9_]+)(?:<[^>]*>)?( \(new pattern\))?", names)
+                     if not m.group(2))
+
+
+def pmc_traffic(role, k, r, nbytes, objects=1, kernels=None, loss=None):
+    """HBM bytes per launch of one role ("encode" / "decode") of a workload from
+    the newest committed PMC pass (tools/pmc_traffic.py: FETCH_SIZE x 2 +
+    WRITE_SIZE, MI355X_MICROARCH.md HBM section; profiles/rNN_vMM ordered by
+    round, then version) -- only when the counted kernels are the ones this call
+    runs (`kernels`, as kernels_for names them) and, for a decode, the counted
+    number of lost originals is this call's (`loss`; a pass without a recorded
+    loss ran tools/kbench.py, which loses min(K, R)); else {} (the line then
+    says traffic: null)."""
     import glob
+    want = kernel_bases(kernels) if kernels else None
     for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*", "pmc_traffic*.json")), key=_profile_order,
                        reverse=True):
         try:
@@ -909,9 +948,14 @@ def pmc_traffic(kernel, k, r, nbytes, objects=1):
         except (OSError, ValueError):
             continue
         key = f"{k}+{r}x{nbytes}" + (f"/batch{objects}" if objects > 1 else "")
-        e = d.get("workloads", {}).get(key, {}).get(kernel)
-        if e:
-            return {"bytes": e["hbm_bytes_per_launch"], "source": os.path.relpath(path, REPO)}
+        e = d.get("workloads", {}).get(key, {}).get(role)
+        if not e:
+            continue
+        if want is not None and kernel_bases(e.get("kernel", "")) != want:
+            continue
+        if role == "decode" and loss is not None and e.get("loss", min(k, r)) != loss:
+            continue
+        return {"bytes": e["hbm_bytes_per_launch"], "source": os.path.relpath(path, REPO), "kernel": e.get("kernel")}
     return {}
 
 

@@ -91,6 +91,7 @@ struct DeviceTables {
     // (release_device_memory) never touches the application's own cached
     // stream-ordered memory in the device's default pool.
     hipMemPool_t pool = nullptr;
+    unsigned cus = 0;  // compute units (grid sizing of persistent kernels and launch-form rules)
     bool ready = false;
 };
 
@@ -132,6 +133,9 @@ LeopardResult ensure_device(int dev, DeviceTables** out) {
         HIP_OK(hipMalloc(reinterpret_cast<void**>(&d.zeros), 4096), "zero page");
         HIP_OK(hipMemset(d.zeros, 0, 4096), "zero page");
         HIP_OK(hipStreamCreateWithFlags(&d.svc, hipStreamNonBlocking), "service stream");
+        int cus = 0;
+        HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev), "compute unit count");
+        d.cus = cus > 0 ? unsigned(cus) : 1u;
         hipMemPoolProps props;
         std::memset(&props, 0, sizeof(props));
         props.allocType = hipMemAllocationTypePinned;
@@ -2111,7 +2115,7 @@ bool run_slab_batch8(int dev, RangeCache& rc, unsigned count, uint64_t bytes, un
             if (form != kFormGeneral && !multi && ff8_bs_supported(T, K, R, b.nchunks) &&
                 (r = c.ws->bs_queue(&q, &qclear)) != Leopard_Success)
                 return r;
-            HIP_OK(launch_ff8_encode_slab(T, b, n, multi, form, c.s, q, qclear), "slab batch kernel");
+            HIP_OK(launch_ff8_encode_slab(T, b, n, multi, form, c.s, c.t->cus, q, qclear), "slab batch kernel");
         }
         return finish(c, false);
     }();
@@ -2206,7 +2210,7 @@ constexpr uint64_t kBatch16SlabBytes = 256ull << 20;
 // 2560-byte pieces: 9.56 vs 8.07 us per object, profiles/r05_v2).
 // LEO_AMD_DEC16_BATCH_ONE=0/1 forces either form in experiment builds.
 constexpr uint64_t kBatch16OneWgsPerCu = 4;
-bool batch16_one_pass(unsigned count, uint64_t bytes) {
+bool batch16_one_pass(unsigned count, uint64_t bytes, unsigned cus) {
 #if LAMD_EXPERIMENT_ENV
     static const int force = [] {
         const char* e = std::getenv("LEO_AMD_DEC16_BATCH_ONE");
@@ -2215,7 +2219,7 @@ bool batch16_one_pass(unsigned count, uint64_t bytes) {
     if (force >= 0) return force == 1;
 #endif
     const uint64_t wgs = (bytes / 8 + 15) / 16 * count;
-    return wgs >= kBatch16OneWgsPerCu * 256;
+    return wgs >= kBatch16OneWgsPerCu * cus;
 }
 LeopardResult decode_batch16(int dev, unsigned count, uint64_t bytes, unsigned K, unsigned R,
                              const void* const* const* orig, const void* const* const* rec, void** const* work) {
@@ -2228,7 +2232,7 @@ LeopardResult decode_batch16(int dev, unsigned count, uint64_t bytes, unsigned K
     const unsigned ntiles_in = (m + K + (1u << kLoBits) - 1) >> kLoBits;
     const unsigned tile0 = m >> kLoBits, nout = ((m + K - 1) >> kLoBits) - tile0 + 1;
     // one pass (round 5): no U slab, one grid (strips, objects); two passes otherwise
-    const bool one = decode16_one_supported(nout) && batch16_one_pass(count, bytes);
+    const bool one = decode16_one_supported(nout) && batch16_one_pass(count, bytes, c.t->cus);
     const uint64_t slab = one ? 0 : (uint64_t(ntiles_in) << kLoBits) * bytes;  // U of one object
     const unsigned per_chunk =
         one ? Workspace::kDec16Slots
@@ -2420,9 +2424,14 @@ LeopardResult decode_batch(unsigned count, uint64_t bytes, unsigned K, unsigned 
             }
             const unsigned m16 = next_pow2(R);
             const unsigned nout16 = ((m16 + K - 1) >> kLoBits) - (m16 >> kLoBits) + 1;
+            DeviceTables* t16 = nullptr;
+            if (on_dev) {
+                const LeopardResult rt = ensure_device(d16, &t16);
+                if (rt != Leopard_Success) return rt;
+            }
             // the two-pass batch keeps a U slab per object: only for pieces under
             // kOnePassMinBytes, where a single object does not fill the GPU
-            if (on_dev && ((decode16_one_supported(nout16) && batch16_one_pass(count, bytes)) ||
+            if (on_dev && ((decode16_one_supported(nout16) && batch16_one_pass(count, bytes, t16->cus)) ||
                            bytes < kOnePassMinBytes))
                 return decode_batch16(d16, count, bytes, K, R, orig, rec, work);
         }

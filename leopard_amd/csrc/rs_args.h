@@ -195,8 +195,9 @@ hipError_t launch_ff8_decode_full(unsigned Tm, const Ff8EncArgs& a, hipStream_t 
 // K = R = m codes, in = received recovery slab, out = outputs).
 // q / qclear: the bit-sliced tile's queue counters for this launch and the set
 // to zero for the next one (Workspace::bs_queue; null: static tile assignment).
+// cus: the device's compute units (sizes the bit-sliced kernel's persistent grid).
 hipError_t launch_ff8_encode_slab(unsigned T, const Ff8SlabBatch& b, unsigned count, bool multi, int form,
-                                  hipStream_t s, uint32_t* q = nullptr, uint32_t* qclear = nullptr);
+                                  hipStream_t s, unsigned cus, uint32_t* q = nullptr, uint32_t* qclear = nullptr);
 hipError_t launch_ff8_decode_batch(unsigned T, const Ff8DecArgs* objs, unsigned count, uint32_t nunits, int mode,
                                    hipStream_t s);
 // Bit-sliced dense tile (rs_ff8_bs.hip): slab batches of K = R = 128 codes,
@@ -204,8 +205,8 @@ hipError_t launch_ff8_decode_batch(unsigned T, const Ff8DecArgs* objs, unsigned 
 bool ff8_bs_supported(unsigned T, unsigned K, unsigned R, unsigned nchunks);
 // Tile queues of the bit-sliced kernel: 8 counters (one per XCD), 128 bytes apart.
 constexpr unsigned kBsQueueDw = 8 * 32;
-hipError_t launch_ff8_bs_slab(const Ff8SlabBatch& b, unsigned count, int form, hipStream_t s, uint32_t* q,
-                              uint32_t* qclear);
+hipError_t launch_ff8_bs_slab(const Ff8SlabBatch& b, unsigned count, int form, hipStream_t s, unsigned cus,
+                              uint32_t* q, uint32_t* qclear);
 
 // Units per lane chosen for each kernel family (the host sizes grids with it).
 constexpr int kUnitsPerLane = 1;

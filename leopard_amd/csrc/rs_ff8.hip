@@ -983,10 +983,10 @@ hipError_t launch_ff8_encode_batch(unsigned T, const Ff8EncArgs* objs, unsigned 
 }
 
 hipError_t launch_ff8_encode_slab(unsigned T, const Ff8SlabBatch& b, unsigned count, bool multi, int form,
-                                  hipStream_t s, uint32_t* q, uint32_t* qclear) {
+                                  hipStream_t s, unsigned cus, uint32_t* q, uint32_t* qclear) {
     // dense 128 + 128 forms: the bit-sliced tile (rs_ff8_bs.hip)
     if (form != kFormGeneral && !multi && bs_tile_enabled() && ff8_bs_supported(T, b.K, b.R, b.nchunks))
-        return launch_ff8_bs_slab(b, count, form, s, q, qclear);
+        return launch_ff8_bs_slab(b, count, form, s, cus, q, qclear);
     hipError_t e = hipErrorInvalidValue;
     static_for<1, 8>([&](auto I) {
         constexpr int TT = decltype(I)::value, RB = batch_bits8(TT);

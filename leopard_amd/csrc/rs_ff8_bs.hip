@@ -344,7 +344,7 @@ LDEV void fused_top(Reg& x) {
 template <int IB, int GBIT, int H>
 LDEV void swap_lanes(Reg& x) {
     static_assert(GBIT == 1 || GBIT == 2, "permlane swaps exist for lane bits 4 and 5");
-#ifdef ABL_XCH
+#if defined(ABL_XCH) || defined(ABL_SWAP)
     return;
 #endif
     static_for<0, 16>([&](auto RI) {
@@ -378,7 +378,7 @@ constexpr unsigned kBsPad = LAMD_BS_SWAPS ? 0u : 1u;
 constexpr unsigned lds_row(unsigned p) { return p + (kBsPad ? (p >> 4) : 0u); }
 template <uint32_t FROM, uint32_t TO>
 LDEV void exchange(Reg& x, uint8_t* area, unsigned g, unsigned l) {
-#ifdef ABL_XCH
+#if defined(ABL_XCH) || defined(ABL_LDSX)
     return;
 #endif
     Reg y;
@@ -655,30 +655,24 @@ bool ff8_bs_supported(unsigned T, unsigned K, unsigned R, unsigned nchunks) {
     return T == 7 && K == 128 && R == 128 && nchunks == 1;
 }
 
-hipError_t launch_ff8_bs_slab(const Ff8SlabBatch& b, unsigned count, int form, hipStream_t s, uint32_t* q,
-                              uint32_t* qclear) {
+hipError_t launch_ff8_bs_slab(const Ff8SlabBatch& b, unsigned count, int form, hipStream_t s, unsigned cus,
+                              uint32_t* q, uint32_t* qclear) {
     if (count == 0 || count > kSlabObjs || (b.nunits * 4u) % 64u != 0 || b.K != 128 || b.R != 128)
         return hipErrorInvalidValue;
     if (form != kFormDenseEnc && form != kFormDenseDec) return hipErrorInvalidValue;
-    static int cus[64] = {};  // compute units per device (queried once)
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return e;
-    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
-    if (cus[dev] == 0) {
-        int n = 0;
-        e = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-        if (e != hipSuccess) return e;
-        cus[dev] = n > 0 ? n : 1;
-    }
+    cus = std::max(cus, 1u);
     uint32_t strips = (b.nunits * 4u + kBsStrip - 1) / kBsStrip;
     uint32_t cnt = count;
     const unsigned total = cnt * strips;
-    const unsigned blocks = std::min<unsigned>((total + kBsWaves - 1) / kBsWaves, unsigned(cus[dev]) * kBsBlocksPerCu);
+    const unsigned blocks = std::min<unsigned>((total + kBsWaves - 1) / kBsWaves, cus * kBsBlocksPerCu);
     const size_t lds = size_t(kBsWaves) * kBsAreaDw * 4;
 #if LAMD_BS_QUEUE == 0
     q = qclear = nullptr;
 #endif
+    // the 8 queues each serve the workgroups of one XCD (blockIdx.x & 7): every
+    // queue needs workgroups, or static assignment (tiles i, i + n, ...); the
+    // next launch's set is still cleared (Workspace::bs_queue alternates them)
+    if (blocks < 8) q = nullptr;
     void* params[] = {const_cast<Ff8SlabBatch*>(&b), &cnt, &strips, &q, &qclear};
     // 32-bit lane offsets when every slab's lane offsets (up to 127 strides + a
     // strip) fit them

@@ -603,7 +603,13 @@ def test_batch_encode_decode_match_oracle(leo, k, r, b, layout):
     recovery pieces.  GF(2^16) objects on narrow strips (m <= 256 encode,
     n <= 2048 decode) also run one grid per kernel; 20 of them span two
     decoder-state chunks (16 erasure patterns a launch pair)."""
-    count = 70 if k == 16 else 20 if k + r > 256 else 5
+    _batch_roundtrip(leo, k, r, b, layout, 70 if k == 16 else 20 if k + r > 256 else 5)
+
+
+def _batch_roundtrip(leo, k, r, b, layout, count):
+    """Encode batch == oracle on every object; decode batch with mixed erasure
+    patterns (even objects full loss, odd ones partial) gives back every lost
+    original."""
     objs = _batch_objects(k, r, b, count, k + r)
     wc, dwc = leo.leo_encode_work_count(k, r), leo.leo_decode_work_count(k, r)
     if layout == "slab":
@@ -644,6 +650,47 @@ def test_batch_encode_decode_match_oracle(leo, k, r, b, layout):
         got = dworks[o].cpu().numpy()
         for i in lo:
             assert np.array_equal(got[i], objs[o][i]), (o, i)
+
+
+@pytest.mark.parametrize("b,count,layout", [(8192, 16, "slab"), (8192, 16, "shuffled"), (64 * 37, 56, "slab"),
+                                            (61440, 3, "slab")])
+def test_batch16_one_pass_grid_matches_oracle(leo, b, count, layout):
+    """GF(2^16) batch decodes whose grid crosses the one-pass rule
+    (leopard_amd.cpp batch16_one_pass: >= 4 workgroups of 16-unit strips per
+    CU): k_dec16n_one_batch over every object in one grid, including a partial
+    last strip (64 x 37-byte pieces: 18.5 strips), shuffled piece orders, and
+    pieces >= 60 KiB in a batch of several objects."""
+    assert (b // 8 + 15) // 16 * count >= 4 * 256
+    _batch_roundtrip(leo, 1000, 200, b, layout, count)
+
+
+_FORCED_BATCH16 = r"""
+import sys
+sys.path.insert(0, {repo!r}); sys.path.insert(0, {tests!r})
+import leopard_amd as leo, test_gpu_parity as t
+assert leo.leo_init() == 0
+for b, count in ((64 * 37, 4), (8192, 16)):
+    t._batch_roundtrip(leo, 1000, 200, b, "slab", count)
+print("forced ok")
+"""
+
+
+@pytest.mark.parametrize("one", ["0", "1"])
+def test_batch16_forced_forms_match_oracle(one):
+    """Both GF(2^16) batch-decode forms on both sides of the one-pass rule:
+    the experiment build (lib/exp, LAMD_EXPERIMENT_ENV) with
+    LEO_AMD_DEC16_BATCH_ONE=0 (two passes, also above the rule) or =1 (one
+    pass, also on small grids with a partial last strip), in a child process."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    repo = os.path.dirname(here)
+    lib = os.path.join(repo, "leopard_amd", "lib", "exp", "libleopard_amd.so")
+    assert os.path.exists(lib), "make -C leopard_amd builds lib/exp"
+    env = dict(os.environ, LEOPARD_AMD_LIB=lib, LEO_AMD_DEC16_BATCH_ONE=one)
+    p = subprocess.run([sys.executable, "-c", _FORCED_BATCH16.format(repo=repo, tests=here)], env=env,
+                       capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0 and "forced ok" in p.stdout, (p.stdout[-2000:], p.stderr[-3000:])
 
 
 @pytest.mark.parametrize("b", [64, 192, 256, 64 * 37, 65536 + 192])

@@ -7,7 +7,9 @@ and each persistent wave's lifetime.
 usage: LEOPARD_AMD_LIB=leopard_amd/exp/<clock build>/libleopard_amd.so python tools/bs_clock.py [OBJ]"""
 import ctypes
 import os
+import subprocess
 import sys
+import threading
 import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -37,12 +39,30 @@ def main():
     bo, bw = mk(sets.p_orig[:cnt]), mk(sets.p_encw[:cnt])
     t0 = time.time()
     n = 0
-    while time.time() - t0 < 2.5:
+    dur = float(os.environ.get("BS_CLOCK_S", "2.5"))
+    samples = []
+
+    def sample():  # BS_CLOCK_SMI=1: board power and clocks under the load (read-only queries)
+        time.sleep(1.0)
+        for cmd in (["amd-smi", "metric", "-p", "-c"], ["rocm-smi", "--showpower", "--showclocks"]):
+            try:
+                samples.append(subprocess.run(cmd, capture_output=True, text=True, timeout=20).stdout)
+            except Exception as e:  # noqa: BLE001
+                samples.append(f"{cmd[0]}: {e}")
+
+    th = threading.Thread(target=sample) if os.environ.get("BS_CLOCK_SMI") else None
+    if th:
+        th.start()
+    while time.time() - t0 < dur:
         buf.zero_()
         for _ in range(20):
             assert lib.leo_amd_encode_batch(cnt, b, k, r, sets.enc_wc, bo, bw) == 0, leo.last_error()
         n += 20
         torch.cuda.synchronize()
+    if th:
+        th.join()
+        for o in samples:
+            print("\n".join(ln for ln in o.splitlines() if ln.strip() and "amdgpu.ids" not in ln)[:3000])
     v = buf.view(ntiles, 4).cpu().double()
     v = v[v[:, 3] > 0]  # one row per persistent wave (indexed by its first tile)
     dc, dr = v[:, 2] - v[:, 0], (v[:, 3] - v[:, 1])

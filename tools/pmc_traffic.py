@@ -81,6 +81,10 @@ def main():
     for kind, e in out.items():
         # encode (K + R) * B; decode (K_surv + R_recv + lost) * B, which is
         # (K + loss) * B when exactly `loss` recovery pieces are received (the benchmark's pattern)
+        if kind == "decode":
+            # originals lost in the counted decodes (kbench.py: the first min(K, R)); bench.py
+            # attaches these bytes only to a decode of the same kernels and loss count
+            e["loss"] = loss if loss is not None else min(k, r)
         if kind == "decode" and loss is not None:
             e["algorithmic_bytes_per_launch"] = objects * (k + loss) * b
         else:

@@ -92,8 +92,31 @@ struct DeviceTables {
     // stream-ordered memory in the device's default pool.
     hipMemPool_t pool = nullptr;
     unsigned cus = 0;  // compute units (grid sizing of persistent kernels and launch-form rules)
+    uint32_t* vtab8 = nullptr;  // FF8 multiply tables by element value (entry 0 all zero; matrix path)
     bool ready = false;
 };
+
+// Coefficient matrices of the GF(2^8) matrix path (rs_ff8_mat.hip), per device,
+// by (kind, K, R, erasure bitmap): the tables of M[i][j] for L outputs x N
+// inputs.  Entries are written once, on the stream of the call that first needs
+// them (event `ready` after the writes), and never rewritten or freed while the
+// process runs: a later call on another stream waits for `ready` on the device
+// (or not at all once it has completed), and no call ever reads an entry that
+// another call could be changing.  At most kMatCacheBytes of tables a device;
+// past that, new patterns take the transform kernels.
+struct MatEntry {
+    uint32_t* tabs = nullptr;
+    unsigned L = 0, N = 0;
+    hipEvent_t ready = nullptr;
+    hipStream_t stream = nullptr;
+    std::atomic<bool> done{false};
+};
+struct MatCache {
+    std::mutex mu;
+    std::map<std::vector<uint32_t>, std::unique_ptr<MatEntry>> entries;
+    size_t bytes = 0;
+};
+constexpr size_t kMatCacheBytes = 64ull << 20;
 
 // Bytes of freed stream-ordered memory the library's pool keeps per device.
 constexpr uint64_t kPoolKeepBytes = 256ull << 20;
@@ -102,6 +125,8 @@ std::mutex g_mu;
 bool g_initialized = false;
 int g_device_count = 0;
 std::vector<DeviceTables> g_dev;
+std::vector<std::unique_ptr<MatCache>> g_mat;  // per device
+std::vector<uint32_t> g_h_vtab8;  // FF8 tables by element value (matrix path)
 std::vector<uint32_t> g_h_tab8, g_h_tab16, g_h_sktab8, g_h_sktab16, g_h_fused8, g_h_fused16, g_h_walsh8, g_h_walsh16,
     g_h_qlog16;
 bool g_q16_ok = false;  // the high part is an XOR-convolution (always; checked at init)
@@ -122,6 +147,7 @@ LeopardResult ensure_device(int dev, DeviceTables** out) {
     DeviceTables& d = g_dev[dev];
     if (!d.ready) {
         HIP_OK(upload(&d.tab8, g_h_tab8), "upload FF8 tables");
+        HIP_OK(upload(&d.vtab8, g_h_vtab8), "upload FF8 value tables");
         HIP_OK(upload(&d.tab16, g_h_tab16), "upload FF16 tables");
         HIP_OK(upload(&d.sktab8, g_h_sktab8), "upload FF8 skew tables");
         HIP_OK(upload(&d.sktab16, g_h_sktab16), "upload FF16 skew tables");
@@ -798,6 +824,31 @@ LeopardResult finish(const Call& c, bool force_sync) {
 
 // --------------------------------------------------------------- encode ----
 
+// ------------------------------------------------------------ matrix path --
+// Small GF(2^8) codes and few losses (rs_ff8_mat.hip): the call applied as its
+// L x N coefficient matrix, built once per (K, R, erasure pattern) from the
+// transform kernels' own outputs on unit pieces.  LEO_AMD_FF8_MATRIX=0 turns it
+// off (A/B experiments); read once.
+bool ff8_matrix_enabled() {
+    static const bool v = !experiment_off("LEO_AMD_FF8_MATRIX");
+    return v;
+}
+thread_local bool tls_mat_gen = false;  // building a matrix: the transform kernels, never the matrix path
+// Where the matrix runs: at most kMatMaxEntries coefficients and kMatMaxWork
+// multiply-adds x bytes a call (beyond that the transforms' fewer operations
+// win over the matrix's shorter critical path).
+constexpr unsigned kMatMaxEntries = 4096;
+constexpr uint64_t kMatMaxWork = 1ull << 27;
+constexpr uint64_t kMatEncodeSmallBytes = 16ull << 10;
+bool use_matrix(unsigned L, unsigned N, uint64_t bytes) {
+    return !tls_mat_gen && ff8_matrix_enabled() && L >= 1 && uint64_t(L) * N <= kMatMaxEntries &&
+           uint64_t(L) * N * bytes <= kMatMaxWork && ff8_mat_supported(L, N);
+}
+LeopardResult encode_matrix(Call& c, uint64_t bytes, uint64_t off, unsigned K, unsigned R, const void* const* orig,
+                            void** work, bool* done);
+LeopardResult decode_matrix(Call& c, uint64_t bytes, uint64_t off, unsigned K, unsigned R, const void* const* orig,
+                            const void* const* rec, void** work, bool* done);
+
 // GF(2^8) encoder argument block of one object: columns [off, off + bytes)
 // of every piece (bytes <= kFf8MaxLaunchBytes).
 void fill_enc8(Ff8EncArgs& a, const DeviceTables* t, unsigned K, unsigned R, const void* const* orig, void** work,
@@ -825,6 +876,13 @@ LeopardResult encode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
     const unsigned nchunks = (K + m - 1) / m;
 
     if (!ff16) {  // n <= 256: one fused kernel, launch data by value (rs_ff8.hip)
+        // small codes: the coefficient matrix, where the transforms run several
+        // chunks one after the other or the call is small (measured: DESIGN.md 7)
+        if (use_matrix(R, K, bytes) && (nchunks >= 3 || bytes <= kMatEncodeSmallBytes)) {
+            bool done = false;
+            const LeopardResult r = encode_matrix(c, bytes, off, K, R, orig, work, &done);
+            if (r != Leopard_Success || done) return r;
+        }
         Ff8EncArgs a;
         // one launch per <= 4 GiB of columns (the kernel counts dword columns in 32 bits)
         for (uint64_t pos = 0; pos < bytes; pos += kFf8MaxLaunchBytes) {
@@ -1072,6 +1130,16 @@ LeopardResult decode_device8(Call& c, uint64_t bytes, uint64_t off, unsigned K, 
         }
         return Leopard_Success;
     }
+    {  // few losses of a small code: the coefficient matrix
+        unsigned L = 0, N = 0;
+        for (unsigned i = 0; i < R; ++i) N += rec[i] != nullptr;
+        for (unsigned i = 0; i < K; ++i) (orig[i] ? N : L) += 1;
+        if (use_matrix(L, N, bytes)) {
+            bool done = false;
+            const LeopardResult r = decode_matrix(c, bytes, off, K, R, orig, rec, work, &done);
+            if (r != Leopard_Success || done) return r;
+        }
+    }
     // the error locator of this pattern (computed on the device once per pattern)
     uint32_t erased[8];
     erasures8(K, R, next_pow2(R), orig, rec, erased);
@@ -1107,6 +1175,131 @@ LeopardResult decode_device8(Call& c, uint64_t bytes, uint64_t off, unsigned K, 
                "decode kernel");
     }
     return Leopard_Success;
+}
+
+// The matrix entry of `key` (L outputs x N inputs) for this call, built now by
+// gen(units, rows, pitch) when new: gen runs the transform kernels on N unit
+// pieces (piece j = the byte 1 at column j, `pitch` bytes each) into L rows,
+// byte j of row i = M[i][j].  *out stays null when the cache is full.
+template <class Gen>
+LeopardResult mat_entry(Call& c, std::vector<uint32_t>&& key, unsigned L, unsigned N, Gen&& gen,
+                        const MatEntry** out) {
+    *out = nullptr;
+    MatCache& mc = *g_mat[c.dev];
+    std::lock_guard<std::mutex> lk(mc.mu);  // generation is a few launches, once per pattern
+    auto it = mc.entries.find(key);
+    if (it != mc.entries.end()) {
+        MatEntry& e = *it->second;
+        if (!e.done.load(std::memory_order_acquire)) {
+            if (hipEventQuery(e.ready) == hipSuccess) e.done.store(true, std::memory_order_release);
+            else HIP_OK(hipStreamWaitEvent(c.s, e.ready, 0), "wait for matrix");  // built on another stream
+        }
+        *out = &e;
+        return Leopard_Success;
+    }
+    const size_t tab_bytes = size_t(L) * N * 32;
+    if (mc.bytes + tab_bytes > kMatCacheBytes) return Leopard_Success;
+    constexpr unsigned kPitch = kFf8Ptrs;  // >= N columns, a multiple of 64 bytes
+    LeopardResult r = c.ws->reserve_device(size_t(N + L) * kPitch);
+    if (r != Leopard_Success) return r;
+    uint8_t* units = c.ws->dbuf;
+    uint8_t* rows = units + size_t(N) * kPitch;
+    HIP_OK(launch_ff8_unit(units, N, kPitch, c.s), "unit pieces");
+    tls_mat_gen = true;
+    r = gen(units, rows, kPitch);
+    tls_mat_gen = false;
+    if (r != Leopard_Success) return r;
+    std::unique_ptr<MatEntry> e(new MatEntry);
+    HIP_OK(pool_alloc(reinterpret_cast<void**>(&e->tabs), tab_bytes, c.dev, c.s), "allocate matrix");
+    HIP_OK(launch_ff8_mat_tabs(rows, kPitch, L, N, c.t->vtab8, e->tabs, c.s), "matrix tables");
+    HIP_OK(hipEventCreateWithFlags(&e->ready, kOrderEvent), "event");
+    HIP_OK(hipEventRecord(e->ready, c.s), "record matrix");
+    e->L = L;
+    e->N = N;
+    e->stream = c.s;
+    mc.bytes += tab_bytes;
+    *out = e.get();
+    mc.entries.emplace(std::move(key), std::move(e));
+    return Leopard_Success;
+}
+
+// out[i] = XOR_j M[i][j] * in[j] over columns [off, off + bytes) (one launch:
+// use_matrix keeps L N bytes <= kMatMaxWork, far below 2^32 dword columns).
+LeopardResult mat_apply(Call& c, const MatEntry& e, const std::vector<uint64_t>& in, const std::vector<uint64_t>& out,
+                        uint64_t bytes, uint64_t off) {
+    Ff8MatArgs a;
+    std::memset(&a, 0, sizeof(a));
+    for (unsigned j = 0; j < e.N; ++j) a.ptr[j] = in[j] + off;
+    for (unsigned i = 0; i < e.L; ++i) a.ptr[e.N + i] = out[i] + off;
+    a.tabs = e.tabs;
+    a.N = e.N;
+    a.L = e.L;
+    a.nunits = uint32_t(bytes / 4);
+    HIP_OK(launch_ff8_mat(a, c.t->cus, c.s), "matrix kernel");
+    return Leopard_Success;
+}
+
+// Encode: recovery j = XOR_i G[j][i] * original i (G depends on K and R only).
+LeopardResult encode_matrix(Call& c, uint64_t bytes, uint64_t off, unsigned K, unsigned R, const void* const* orig,
+                            void** work, bool* done) {
+    *done = false;
+    const MatEntry* e = nullptr;
+    LeopardResult r = mat_entry(c, {0u, K, R}, R, K,
+                                [&](uint8_t* units, uint8_t* rows, unsigned pitch) {
+                                    std::vector<const void*> o(K);
+                                    std::vector<void*> w(R);
+                                    for (unsigned i = 0; i < K; ++i) o[i] = units + size_t(i) * pitch;
+                                    for (unsigned j = 0; j < R; ++j) w[j] = rows + size_t(j) * pitch;
+                                    return encode_device(c, pitch, 0, K, R, o.data(), w.data());
+                                },
+                                &e);
+    if (r != Leopard_Success || !e) return r;
+    std::vector<uint64_t> in(K), out(R);
+    for (unsigned i = 0; i < K; ++i) in[i] = uint64_t(reinterpret_cast<uintptr_t>(orig[i]));
+    for (unsigned j = 0; j < R; ++j) out[j] = uint64_t(reinterpret_cast<uintptr_t>(work[j]));
+    r = mat_apply(c, *e, in, out, bytes, off);
+    *done = r == Leopard_Success;
+    return r;
+}
+
+// Decode of one erasure pattern: lost original i = XOR_j D[i][j] * received j,
+// over every received piece (recovery pieces in index order, then originals):
+// the transform decoder's own map (rs_ff8.hip kernels on unit pieces), also on
+// inputs that are not codewords.
+LeopardResult decode_matrix(Call& c, uint64_t bytes, uint64_t off, unsigned K, unsigned R, const void* const* orig,
+                            const void* const* rec, void** work, bool* done) {
+    *done = false;
+    std::vector<uint64_t> in, out;
+    for (unsigned i = 0; i < R; ++i)
+        if (rec[i]) in.push_back(uint64_t(reinterpret_cast<uintptr_t>(rec[i])));
+    for (unsigned i = 0; i < K; ++i) {
+        if (orig[i]) in.push_back(uint64_t(reinterpret_cast<uintptr_t>(orig[i])));
+        else out.push_back(uint64_t(reinterpret_cast<uintptr_t>(work[i])));
+    }
+    const unsigned N = unsigned(in.size()), L = unsigned(out.size());
+    uint32_t erased[8];
+    erasures8(K, R, next_pow2(R), orig, rec, erased);
+    std::vector<uint32_t> key{1u, K, R};
+    key.insert(key.end(), erased, erased + 8);
+    const MatEntry* e = nullptr;
+    LeopardResult r = mat_entry(c, std::move(key), L, N,
+                                [&](uint8_t* units, uint8_t* rows, unsigned pitch) {
+                                    std::vector<const void*> ou(K), ru(R);
+                                    std::vector<void*> wu(K);
+                                    unsigned j = 0, l = 0;
+                                    for (unsigned i = 0; i < R; ++i)
+                                        ru[i] = rec[i] ? units + size_t(j++) * pitch : nullptr;
+                                    for (unsigned i = 0; i < K; ++i) {
+                                        ou[i] = orig[i] ? units + size_t(j++) * pitch : nullptr;
+                                        wu[i] = orig[i] ? nullptr : rows + size_t(l++) * pitch;
+                                    }
+                                    return decode_device8(c, pitch, 0, K, R, ou.data(), ru.data(), wu.data());
+                                },
+                                &e);
+    if (r != Leopard_Success || !e) return r;
+    r = mat_apply(c, *e, in, out, bytes, off);
+    *done = r == Leopard_Success;
+    return r;
 }
 
 // GF(2^16) decoder state of one erasure pattern (a workspace slot): erasure
@@ -2471,6 +2664,10 @@ LEO_EXPORT int leo_init_(int version) {
     const GaloisField& f8 = field8();
     const GaloisField& f16 = field16();
     build_perm_tables8(f8, g_h_tab8);
+    g_h_vtab8.assign(256 * kTab8Dwords, 0u);  // entry v = the table of log_of[v]; entry 0 stays zero
+    for (unsigned v = 1; v < 256; ++v)
+        std::copy_n(g_h_tab8.begin() + size_t(f8.log_of[v]) * kTab8Dwords, kTab8Dwords,
+                    g_h_vtab8.begin() + size_t(v) * kTab8Dwords);
     build_perm_tables16(f16, g_h_tab16);
     build_skew_tables(f8, g_h_tab8, kTab8Dwords, kSkewFlagDw8, g_h_sktab8);
     build_skew_tables(f16, g_h_tab16, kTab16Dwords, kSkewFlagDw16, g_h_sktab16);
@@ -2480,6 +2677,8 @@ LEO_EXPORT int leo_init_(int version) {
     g_h_walsh16.assign(f16.log_walsh.begin(), f16.log_walsh.end());
     g_q16_ok = build_high_q16(f16, g_h_qlog16);
     g_dev.assign(count, DeviceTables{});
+    g_mat.clear();
+    for (int i = 0; i < count; ++i) g_mat.emplace_back(new MatCache);
     g_device_count = count;
     g_initialized = true;
     std::atexit([] { g_exiting.store(true); });  // after the runtime's own registration: runs before its teardown

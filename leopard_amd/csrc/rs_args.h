@@ -114,6 +114,17 @@ struct Ff8DecArgs {
     uint32_t dense;                // half decoder with K = R = m, every recovery received (host-side dispatch)
     __host__ __device__ uint64_t piece(unsigned i) const { return ptr[i]; }
 };
+// GF(2^8) codes applied as their coefficient matrix (rs_ff8_mat.hip): output
+// i = XOR_j M[i][j] * input j, for L <= kFf8MatMaxOut outputs and N inputs
+// (N + L <= kFf8Ptrs); tabs: L x N byte-permute multiply tables, 8 dwords per
+// entry (FF8::Tab in dwords 0-4), row-major by output.
+constexpr unsigned kFf8MatMaxOut = 32;
+struct Ff8MatArgs {
+    uint64_t ptr[kFf8Ptrs];  // [0, N) inputs, [N, N + L) outputs (column base applied)
+    const uint32_t* tabs;
+    unsigned N, L;
+    uint32_t nunits;         // dword columns in this launch
+};
 // GF(2^8) error locators of up to kEl8Jobs erasure patterns in one launch
 // (k_el8): job i writes the 256 el bytes of bitmap erased (LeopardFF8.cpp:
 // 1825-1840) to out + 64 * slot dwords.
@@ -207,6 +218,15 @@ bool ff8_bs_supported(unsigned T, unsigned K, unsigned R, unsigned nchunks);
 constexpr unsigned kBsQueueDw = 8 * 32;
 hipError_t launch_ff8_bs_slab(const Ff8SlabBatch& b, unsigned count, int form, hipStream_t s, unsigned cus,
                               uint32_t* q, uint32_t* qclear);
+
+// Matrix path (rs_ff8_mat.hip): the kernel, unit pieces (piece j = byte 1 at
+// column j, `pitch` bytes each) and the conversion of the L rows of products
+// (byte j of row i = M[i][j]) into tables, through vtab (value-indexed tables).
+bool ff8_mat_supported(unsigned L, unsigned N);
+hipError_t launch_ff8_mat(const Ff8MatArgs& a, unsigned cus, hipStream_t s);
+hipError_t launch_ff8_unit(uint8_t* out, unsigned n, unsigned pitch, hipStream_t s);
+hipError_t launch_ff8_mat_tabs(const uint8_t* rows, unsigned pitch, unsigned L, unsigned N, const uint32_t* vtab,
+                               uint32_t* tabs, hipStream_t s);
 
 // Units per lane chosen for each kernel family (the host sizes grids with it).
 constexpr int kUnitsPerLane = 1;

@@ -124,6 +124,98 @@ def test_decode_roundtrip_and_oracle(leo, k, r, b, loss):
         assert np.array_equal(got[i], expect[i]), i
 
 
+# The GF(2^8) matrix path (rs_ff8_mat.hip, leopard_amd.cpp use_matrix): small codes and few
+# losses run as the L x N coefficient matrix built from the transform kernels' outputs on
+# unit pieces.  Shapes on it (the breadth lines 100+10 / 100+20, the 16-loss headline shape,
+# output groups of 4 and 8, lost recovery pieces), each encode and decode repeated so
+# the second call reads the cached matrix.
+MAT_CASES = [(100, 10, 2560, 10, 0), (100, 20, 2560, 20, 0), (128, 128, 65536, 16, 0), (64, 32, 4096, 16, 5),
+             (32, 8, 65536, 4, 2), (16, 16, 64, 1, 3), (200, 30, 256, 29, 0), (7, 5, 64 * 9, 3, 1)]
+
+
+@pytest.mark.parametrize("k,r,b,loss,rec_lost", MAT_CASES)
+def test_matrix_path_matches_oracle(leo, k, r, b, loss, rec_lost):
+    rng = np.random.default_rng(k * 5 + r * 3 + b + loss)
+    data = rng.integers(0, 256, (k, b), dtype=np.uint8)
+    expect = ol.oracle().encode(data, r)
+    for _ in range(2):
+        assert np.array_equal(gpu_encode(leo, data, r), expect)
+    lost_o = sorted(rng.choice(k, loss, replace=False).tolist())
+    # r - loss recovery pieces are needed at least; rec_lost of the others are missing too
+    lost_r = sorted(rng.choice(r, min(rec_lost, r - loss), replace=False).tolist())
+    for _ in range(2):
+        got = gpu_decode(leo, data, expect, lost_o, lost_r)
+        for i in lost_o:
+            assert np.array_equal(got[i], data[i]), i
+    junk = rng.integers(0, 256, (r, b), dtype=np.uint8)  # not a codeword: the exact decoder map
+    want = ol.oracle().decode(data, junk, lost_o, lost_r)
+    got = gpu_decode(leo, data, junk, lost_o, lost_r)
+    for i in lost_o:
+        assert np.array_equal(got[i], want[i]), i
+
+
+def test_matrix_built_on_one_stream_used_on_another(leo):
+    """A matrix generated by a call on stream A and used at once by an async call
+    on stream B (B waits for A's generation on the device, no host sync)."""
+    k, r, b, loss = 90, 17, 4096, 11
+    rng = np.random.default_rng(17)
+    data = rng.integers(0, 256, (k, b), dtype=np.uint8)
+    rec = ol.oracle().encode(data, r)
+    lost_o = sorted(rng.choice(k, loss, replace=False).tolist())
+    lost_r = sorted(rng.choice(r, 2, replace=False).tolist())
+    orig, recd = dev_tensor(data), dev_tensor(rec)
+    torch.cuda.synchronize()
+    outs = []
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    leo.set_async(True)
+    try:
+        for st in (sa, sb):
+            leo.set_stream(st.cuda_stream)
+            with torch.cuda.stream(st):
+                outs.append(leo.decode(orig, recd, lost_o, lost_r))
+    finally:
+        leo.set_async(False)
+        leo.set_stream(None)
+    torch.cuda.synchronize()
+    for o in outs:
+        for i in lost_o:
+            assert np.array_equal(o[i].cpu().numpy(), data[i]), i
+
+
+_TRANSFORM_ONLY = r"""
+import sys
+sys.path.insert(0, {repo!r}); sys.path.insert(0, {tests!r})
+import leopard_amd as leo, test_gpu_parity as t
+assert leo.leo_init() == 0
+n = 0
+for k, r, b in t.ENC_CASES:
+    if k + r <= 256:
+        t.test_encode_matches_oracle(leo, k, r, b); n += 1
+for k, r, b, loss in t.DEC_CASES:
+    if k + r <= 256:
+        t.test_decode_roundtrip_and_oracle(leo, k, r, b, loss); n += 1
+for c in t.MAT_CASES:
+    t.test_matrix_path_matches_oracle(leo, *c); n += 1
+print("transform ok", n)
+"""
+
+
+def test_ff8_transform_kernels_with_matrix_path_off():
+    """The GF(2^8) shapes of ENC_CASES / DEC_CASES / MAT_CASES through the transform
+    kernels alone (experiment build, LEO_AMD_FF8_MATRIX=0), in a child process:
+    the product routes many of them to the matrix path, which is built from
+    these kernels."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    repo = os.path.dirname(here)
+    lib = os.path.join(repo, "leopard_amd", "lib", "exp", "libleopard_amd.so")
+    env = dict(os.environ, LEOPARD_AMD_LIB=lib, LEO_AMD_FF8_MATRIX="0")
+    p = subprocess.run([sys.executable, "-c", _TRANSFORM_ONLY.format(repo=repo, tests=here)], env=env,
+                       capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0 and "transform ok" in p.stdout, (p.stdout[-2000:], p.stderr[-3000:])
+
+
 # The single-pass GF(2^16) decoder (k_dec16n_one: n <= 2048, <= 4 tiles of originals,
 # pieces >= 60 KiB): a tile mixing recovery and original positions (m = 128), a last
 # column strip of 8 units (B = 64 mod 128) in the 16-unit form and of one 64-byte

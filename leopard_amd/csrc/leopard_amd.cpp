@@ -834,15 +834,21 @@ bool ff8_matrix_enabled() {
     return v;
 }
 thread_local bool tls_mat_gen = false;  // building a matrix: the transform kernels, never the matrix path
-// Where the matrix runs: at most kMatMaxEntries coefficients and kMatMaxWork
-// multiply-adds x bytes a call (beyond that the transforms' fewer operations
-// win over the matrix's shorter critical path).
+// Where the matrix runs (measured crossovers): at most
+// kMatMaxEntries coefficients, and L N bytes (the matrix's multiply-adds) at
+// most kMatMaxWork where the transform path is slow for its work -- the split
+// decoder (n = 2m, its three transforms and 128 scale multiplies) and encoders
+// that run three or more chunks one after the other -- or any call of at most
+// kMatSmallBytes; kMatMaxWorkOther otherwise.
 constexpr unsigned kMatMaxEntries = 4096;
 constexpr uint64_t kMatMaxWork = 1ull << 27;
-constexpr uint64_t kMatEncodeSmallBytes = 16ull << 10;
-bool use_matrix(unsigned L, unsigned N, uint64_t bytes) {
+constexpr uint64_t kMatMaxWorkOther = 1ull << 25;
+constexpr uint64_t kMatSmallBytes = 16ull << 10;
+bool use_matrix(unsigned L, unsigned N, uint64_t bytes, bool slow_transform) {
+    const uint64_t work = uint64_t(L) * N * bytes;
     return !tls_mat_gen && ff8_matrix_enabled() && L >= 1 && uint64_t(L) * N <= kMatMaxEntries &&
-           uint64_t(L) * N * bytes <= kMatMaxWork && ff8_mat_supported(L, N);
+           work <= (slow_transform || bytes <= kMatSmallBytes ? kMatMaxWork : kMatMaxWorkOther) &&
+           ff8_mat_supported(L, N);
 }
 LeopardResult encode_matrix(Call& c, uint64_t bytes, uint64_t off, unsigned K, unsigned R, const void* const* orig,
                             void** work, bool* done);
@@ -876,9 +882,8 @@ LeopardResult encode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
     const unsigned nchunks = (K + m - 1) / m;
 
     if (!ff16) {  // n <= 256: one fused kernel, launch data by value (rs_ff8.hip)
-        // small codes: the coefficient matrix, where the transforms run several
-        // chunks one after the other or the call is small (measured: DESIGN.md 7)
-        if (use_matrix(R, K, bytes) && (nchunks >= 3 || bytes <= kMatEncodeSmallBytes)) {
+        // small codes: the coefficient matrix (use_matrix)
+        if (use_matrix(R, K, bytes, nchunks >= 3) && (nchunks >= 2 || bytes <= kMatSmallBytes)) {
             bool done = false;
             const LeopardResult r = encode_matrix(c, bytes, off, K, R, orig, work, &done);
             if (r != Leopard_Success || done) return r;
@@ -1134,7 +1139,9 @@ LeopardResult decode_device8(Call& c, uint64_t bytes, uint64_t off, unsigned K, 
         unsigned L = 0, N = 0;
         for (unsigned i = 0; i < R; ++i) N += rec[i] != nullptr;
         for (unsigned i = 0; i < K; ++i) (orig[i] ? N : L) += 1;
-        if (use_matrix(L, N, bytes)) {
+        const unsigned m = next_pow2(R);
+        const bool split = L < K && 2 * m == next_pow2(m + K);  // the split decoder's shape (fill_dec8)
+        if (use_matrix(L, N, bytes, split)) {
             bool done = false;
             const LeopardResult r = decode_matrix(c, bytes, off, K, R, orig, rec, work, &done);
             if (r != Leopard_Success || done) return r;

@@ -37,11 +37,14 @@ namespace {
 constexpr int kMatWaves = 16;  // most waves per workgroup (inputs split across them)
 constexpr int kMatInMax = 16;  // most inputs per wave (the launch sizes the workgroup for it)
 
-// C dwords of a piece from byte offset `off` (nontemporal: each byte is read once)
+// C dwords of a piece from byte offset `off`: plain (cached) loads -- the
+// workgroups of the other output groups of this strip read the same bytes,
+// from the same XCD's L2 (workgroup ids y * strips + x, strips a multiple of 8
+// or close: the groups of strip x land on one XCD)
 template <int C>
 LDEV void mat_load(uint32_t* v, uint64_t base, uint32_t off) {
     using V = typename VecT<C>::type;
-    const V x = __builtin_nontemporal_load(gptr<const V>(reinterpret_cast<const uint8_t*>(base) + off));
+    const V x = *gptr<const V>(reinterpret_cast<const uint8_t*>(base) + off);
     if constexpr (C == 1) v[0] = x;
     else { v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w; }
 }

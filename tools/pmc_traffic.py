@@ -22,9 +22,9 @@ from collections import defaultdict
 def kernel_kind(name):
     # the GF(2^8) encoder tile also runs full-loss decodes of K = R = m codes:
     # its last template argument is the form (rs_args.h: 1 dense encode, 2 dense decode)
-    m = re.search(r"k_ff8_bs_slab<([^>]*)>", name)  # bit-sliced dense tile: form 1 encode, 2 decode
+    m = re.search(r"k_ff8_bs_slab<([^>]*)>", name)  # bit-sliced dense tile: form (first argument) 1 encode, 2 decode
     if m:
-        return "decode" if m.group(1).strip() == "2" else "encode"
+        return "decode" if m.group(1).split(",")[0].strip() == "2" else "encode"
     m = re.search(r"k_ff8_enc(?:_slab|_batch)?<([^>]*)>", name)
     if m:
         return "decode" if m.group(1).split(",")[-1].strip() == "2" else "encode"

@@ -834,7 +834,7 @@ bool ff8_matrix_enabled() {
     return v;
 }
 thread_local bool tls_mat_gen = false;  // building a matrix: the transform kernels, never the matrix path
-// Where the matrix runs (measured crossovers, DESIGN.md section 7.0): at most
+// Where the matrix runs (measured crossovers, DESIGN.md section 7.6): at most
 // kMatMaxEntries coefficients, and L N bytes (the matrix's multiply-adds) at
 // most kMatMaxWork where the transform path is slow for its work -- the split
 // decoder (n = 2m, its three transforms and 128 scale multiplies) and encoders

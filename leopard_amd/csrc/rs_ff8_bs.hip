@@ -561,9 +561,10 @@ LDEV void low_layers(Reg& x, const uint32_t (&G)[3]) {
 // lane swaps): the last FFT layers, transposes and stores of half 0 run, then
 // the next tile's half-0 loads are issued into the freed registers while half 1
 // computes; at the top of the next tile half 1's loads are in flight while half
-// 0 transposes and runs its IFFT layers.  (Prefetching part of the next tile a
-// whole tile ahead -- by LDS-DMA into the unused LDS, or into spare VGPRs --
-// measured no faster: the kernel runs at a power-limited clock)
+// 0 transposes and runs its IFFT layers.  (Deeper prefetch -- part of the next
+// tile a whole tile ahead, by LDS-DMA into the unused LDS or into spare VGPRs --
+// addresses latency, which is not what binds: the kernel runs at the board's
+// power limit, memory and arithmetic each at full clock alone)
 template <int kForm, bool kNarrow>
 __global__ void __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(LAMD_BS_OCC, LAMD_BS_OCC)))
 k_ff8_bs_slab(Ff8SlabBatch b, uint32_t count, uint32_t strips, uint32_t* q, uint32_t* qclear) {

@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "rs_args.h"
 
@@ -46,6 +47,7 @@ LDEV void mat_load(uint32_t* v, uint64_t base, uint32_t off) {
     using V = typename VecT<C>::type;
     const V x = *gptr<const V>(reinterpret_cast<const uint8_t*>(base) + off);
     if constexpr (C == 1) v[0] = x;
+    else if constexpr (C == 2) { v[0] = x.x; v[1] = x.y; }
     else { v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w; }
 }
 template <int C>
@@ -53,6 +55,7 @@ LDEV void mat_store(uint64_t base, uint32_t off, const uint32_t* v) {
     using V = typename VecT<C>::type;
     V x;
     if constexpr (C == 1) x = v[0];
+    else if constexpr (C == 2) x = V{v[0], v[1]};
     else x = V{v[0], v[1], v[2], v[3]};
     __builtin_nontemporal_store(x, gptr<V>(reinterpret_cast<uint8_t*>(base) + off));
 }
@@ -175,10 +178,18 @@ hipError_t launch_ff8_mat(const Ff8MatArgs& a, unsigned cus, hipStream_t s) {
     if (!ff8_mat_supported(a.L, a.N) || a.nunits == 0) return hipErrorInvalidValue;
     auto groups = [&](unsigned lb) { return (a.L + lb - 1) / lb; };
     const unsigned strips4 = (a.nunits + 255) / 256;
-    const unsigned c = strips4 * groups(2) >= cus ? 4u : 1u;
+    unsigned c = strips4 * groups(2) >= cus ? 4u : 1u;
+#if LAMD_EXPERIMENT_ENV
+    static const int force_c = [] { const char* e = std::getenv("LEO_AMD_MAT_C"); return e ? std::atoi(e) : 0; }();
+    if (force_c == 1 || force_c == 2 || force_c == 4) c = unsigned(force_c);
+#endif
     const unsigned strips = (a.nunits + 64 * c - 1) / (64 * c);
     unsigned lb = c == 4 ? 4 : 8;
     while (lb > 1 && strips * groups(lb) < cus) lb /= 2;
+#if LAMD_EXPERIMENT_ENV
+    static const int force_lb = [] { const char* e = std::getenv("LEO_AMD_MAT_LB"); return e ? std::atoi(e) : 0; }();
+    if (force_lb == 1 || force_lb == 2 || force_lb == 4 || (force_lb == 8 && c <= 2)) lb = unsigned(force_lb);
+#endif
     // every wave of the workgroup in use even for few inputs: a small call is
     // bound by the chain through one wave (measured: 16 waves of 1-2 inputs beat
     // 2 waves of 12), a large one by the total instructions, which W barely changes
@@ -191,6 +202,11 @@ hipError_t launch_ff8_mat(const Ff8MatArgs& a, unsigned cus, hipStream_t s) {
         fn = lb == 4   ? reinterpret_cast<const void*>(&k_ff8_mat<4, 4>)
              : lb == 2 ? reinterpret_cast<const void*>(&k_ff8_mat<2, 4>)
                        : reinterpret_cast<const void*>(&k_ff8_mat<1, 4>);
+    else if (c == 2)
+        fn = lb == 8   ? reinterpret_cast<const void*>(&k_ff8_mat<8, 2>)
+             : lb == 4 ? reinterpret_cast<const void*>(&k_ff8_mat<4, 2>)
+             : lb == 2 ? reinterpret_cast<const void*>(&k_ff8_mat<2, 2>)
+                       : reinterpret_cast<const void*>(&k_ff8_mat<1, 2>);
     else
         fn = lb == 8   ? reinterpret_cast<const void*>(&k_ff8_mat<8, 1>)
              : lb == 4 ? reinterpret_cast<const void*>(&k_ff8_mat<4, 1>)

@@ -852,6 +852,41 @@ bool use_matrix(unsigned L, unsigned N, uint64_t bytes, bool slow_transform) {
 }
 LeopardResult encode_matrix(Call& c, uint64_t bytes, uint64_t off, unsigned K, unsigned R, const void* const* orig,
                             void** work, bool* done);
+bool slab_of(const void* const* p, unsigned n, uint64_t& base, int32_t& stride);
+
+// Single dense 128 + 128 calls (encode, or the full-loss decode) on pieces of at
+// least kBsSingleMinBytes whose inputs and outputs are slabs: the bit-sliced
+// batch tile with one object (rs_ff8_bs.hip; its persistent grid has a tile for
+// every wave from 2048 256-byte strips on).  Smaller calls keep the byte tile,
+// whose 16-wave workgroups finish one strip sooner.  *done: launched.
+constexpr uint64_t kBsSingleMinBytes = 512ull << 10;
+LeopardResult dense_single_bs(Call& c, uint64_t bytes, uint64_t off, unsigned m, const void* const* in,
+                              void* const* out, int form, bool* done) {
+    *done = false;
+    uint64_t ib = 0, ob = 0;
+    int32_t is = 0, os = 0;
+    static const bool enabled = !experiment_off("LEO_AMD_FF8_BS_SINGLE");  // A/B experiments only
+    if (!enabled || m != 128 || bytes < kBsSingleMinBytes || bytes / 4 > 0xFFFFFFFFull || !ff8_bs_supported(7, m, m, 1) ||
+        !slab_of(in, m, ib, is) || !slab_of(const_cast<const void* const*>(out), m, ob, os))
+        return Leopard_Success;
+    Ff8SlabBatch b;
+    std::memset(&b, 0, sizeof(b));
+    b.in_base[0] = ib + off;
+    b.in_stride[0] = is;
+    b.out_base[0] = ob + off;
+    b.out_stride[0] = os;
+    b.sktab = c.t->sktab8;
+    b.fused = c.t->fused8 + size_t(6) * 256 * kTab8Dwords;  // T = 7, chunk 0
+    b.K = b.R = m;
+    b.nchunks = 1;
+    b.nunits = uint32_t(bytes / 4);
+    uint32_t *q = nullptr, *qclear = nullptr;
+    const LeopardResult r = c.ws->bs_queue(&q, &qclear);
+    if (r != Leopard_Success) return r;
+    HIP_OK(launch_ff8_encode_slab(7, b, 1, false, form, c.s, c.t->cus, q, qclear), "bit-sliced single call");
+    *done = true;
+    return Leopard_Success;
+}
 LeopardResult decode_matrix(Call& c, uint64_t bytes, uint64_t off, unsigned K, unsigned R, const void* const* orig,
                             const void* const* rec, void** work, bool* done);
 
@@ -883,6 +918,11 @@ LeopardResult encode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
 
     if (!ff16) {  // n <= 256: one fused kernel, launch data by value (rs_ff8.hip)
         // small codes: the coefficient matrix (use_matrix)
+        if (K == R && nchunks == 1) {  // dense 128 + 128 on large pieces: the bit-sliced tile
+            bool done = false;
+            const LeopardResult r = dense_single_bs(c, bytes, off, m, orig, work, kFormDenseEnc, &done);
+            if (r != Leopard_Success || done) return r;
+        }
         if (use_matrix(R, K, bytes, nchunks >= 3) && (nchunks >= 2 || bytes <= kMatSmallBytes)) {
             bool done = false;
             const LeopardResult r = encode_matrix(c, bytes, off, K, R, orig, work, &done);
@@ -1128,6 +1168,9 @@ LeopardResult decode_device8(Call& c, uint64_t bytes, uint64_t off, unsigned K, 
                              const void* const* rec, void** work) {
     const unsigned Tn = log2u(next_pow2(next_pow2(R) + K));
     if (full_loss_square(K, R, orig, rec)) {
+        bool done = false;
+        LeopardResult r = dense_single_bs(c, bytes, off, R, rec, work, kFormDenseDec, &done);
+        if (r != Leopard_Success || done) return r;
         Ff8EncArgs e;
         for (uint64_t pos = 0; pos < bytes; pos += kFf8MaxLaunchBytes) {
             fill_dec8_full(e, c.t, R, rec, work, off + pos, std::min(kFf8MaxLaunchBytes, bytes - pos));

@@ -813,6 +813,23 @@ def test_bitsliced_dense_tile_matches_oracle(leo, b):
         assert torch.equal(dworks[o][:k], dev[o]), o
 
 
+@pytest.mark.parametrize("b", [(512 << 10) + 192, 1 << 20])
+def test_bitsliced_single_dense_calls(leo, b):
+    """Single leo_encode / full-loss leo_decode calls of 128 + 128 codes on pieces
+    of >= 512 KiB laid out as slabs run the bit-sliced tile as a one-object batch
+    (leopard_amd.cpp dense_single_bs): encode against the oracle (a partial last
+    strip at + 192 bytes), the full-loss decode back to the originals."""
+    k = r = 128
+    rng = np.random.default_rng(b)
+    data = rng.integers(0, 256, (k, b), dtype=np.uint8)
+    expect = ol.oracle().encode(data, r)
+    got = gpu_encode(leo, data, r)
+    assert np.array_equal(got, expect)
+    dec = gpu_decode(leo, data, expect, list(range(k)), [])
+    for i in range(k):
+        assert np.array_equal(dec[i], data[i]), i
+
+
 def test_bitsliced_headline_geometry(leo):
     """The benchmark's own launch: ONE encode-batch and ONE decode-batch launch
     over 64 objects of 128 + 128 x 65536 B laid out as slabs (bench.py

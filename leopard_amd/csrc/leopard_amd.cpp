@@ -839,15 +839,23 @@ thread_local bool tls_mat_gen = false;  // building a matrix: the transform kern
 // most kMatMaxWork where the transform path is slow for its work -- the split
 // decoder (n = 2m, its three transforms and 128 scale multiplies) and encoders
 // that run three or more chunks one after the other -- or any call of at most
-// kMatSmallBytes; kMatMaxWorkOther otherwise.
+// kMatSmallBytes; kMatMaxWorkOther otherwise.  Decodes (their transform path
+// runs the error locator, two or three transforms and the scale multiplies):
+// kMatMaxWorkDec.
 constexpr unsigned kMatMaxEntries = 4096;
 constexpr uint64_t kMatMaxWork = 1ull << 27;
 constexpr uint64_t kMatMaxWorkOther = 1ull << 25;
+constexpr uint64_t kMatMaxWorkDec = 3ull << 27;
 constexpr uint64_t kMatSmallBytes = 16ull << 10;
-bool use_matrix(unsigned L, unsigned N, uint64_t bytes, bool slow_transform) {
+bool use_matrix(unsigned L, unsigned N, uint64_t bytes, bool slow_transform, bool decode) {
     const uint64_t work = uint64_t(L) * N * bytes;
-    return !tls_mat_gen && ff8_matrix_enabled() && L >= 1 && uint64_t(L) * N <= kMatMaxEntries &&
-           work <= (slow_transform || bytes <= kMatSmallBytes ? kMatMaxWork : kMatMaxWorkOther) &&
+    uint64_t cap = decode ? kMatMaxWorkDec : slow_transform || bytes <= kMatSmallBytes ? kMatMaxWork : kMatMaxWorkOther;
+#if LAMD_EXPERIMENT_ENV
+    // A/B of the crossovers: LEO_AMD_MAT_WORK=s sets both caps to 2^s
+    static const int work_log2 = [] { const char* e = std::getenv("LEO_AMD_MAT_WORK"); return e ? std::atoi(e) : 0; }();
+    if (work_log2 > 0 && work_log2 < 40) cap = 1ull << work_log2;
+#endif
+    return !tls_mat_gen && ff8_matrix_enabled() && L >= 1 && uint64_t(L) * N <= kMatMaxEntries && work <= cap &&
            ff8_mat_supported(L, N);
 }
 LeopardResult encode_matrix(Call& c, uint64_t bytes, uint64_t off, unsigned K, unsigned R, const void* const* orig,
@@ -923,7 +931,7 @@ LeopardResult encode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
             const LeopardResult r = dense_single_bs(c, bytes, off, m, orig, work, kFormDenseEnc, &done);
             if (r != Leopard_Success || done) return r;
         }
-        if (use_matrix(R, K, bytes, nchunks >= 3) && (nchunks >= 2 || bytes <= kMatSmallBytes)) {
+        if (use_matrix(R, K, bytes, nchunks >= 3, false) && (nchunks >= 2 || bytes <= kMatSmallBytes)) {
             bool done = false;
             const LeopardResult r = encode_matrix(c, bytes, off, K, R, orig, work, &done);
             if (r != Leopard_Success || done) return r;
@@ -1182,9 +1190,7 @@ LeopardResult decode_device8(Call& c, uint64_t bytes, uint64_t off, unsigned K, 
         unsigned L = 0, N = 0;
         for (unsigned i = 0; i < R; ++i) N += rec[i] != nullptr;
         for (unsigned i = 0; i < K; ++i) (orig[i] ? N : L) += 1;
-        const unsigned m = next_pow2(R);
-        const bool split = L < K && 2 * m == next_pow2(m + K);  // the split decoder's shape (fill_dec8)
-        if (use_matrix(L, N, bytes, split)) {
+        if (use_matrix(L, N, bytes, true, true)) {
             bool done = false;
             const LeopardResult r = decode_matrix(c, bytes, off, K, R, orig, rec, work, &done);
             if (r != Leopard_Success || done) return r;
@@ -1247,7 +1253,7 @@ LeopardResult mat_entry(Call& c, std::vector<uint32_t>&& key, unsigned L, unsign
         *out = &e;
         return Leopard_Success;
     }
-    const size_t tab_bytes = size_t(L) * N * 32;
+    const size_t tab_bytes = (size_t(L) * N + 1) * 32;  // + one zero entry (k_ff8_mat's empty slots)
     if (mc.bytes + tab_bytes > kMatCacheBytes) return Leopard_Success;
     constexpr unsigned kPitch = kFf8Ptrs;  // >= N columns, a multiple of 64 bytes
     LeopardResult r = c.ws->reserve_device(size_t(N + L) * kPitch);

@@ -117,7 +117,7 @@ struct Ff8DecArgs {
 // GF(2^8) codes applied as their coefficient matrix (rs_ff8_mat.hip): output
 // i = XOR_j M[i][j] * input j, for L <= kFf8MatMaxOut outputs and N inputs
 // (N + L <= kFf8Ptrs); tabs: L x N byte-permute multiply tables, 8 dwords per
-// entry (FF8::Tab in dwords 0-4), row-major by output.
+// entry (FF8::Tab in dwords 0-4), row-major by output, then one all-zero entry.
 constexpr unsigned kFf8MatMaxOut = 32;
 struct Ff8MatArgs {
     uint64_t ptr[kFf8Ptrs];  // [0, N) inputs, [N, N + L) outputs (column base applied)

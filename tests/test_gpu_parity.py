@@ -132,7 +132,8 @@ def test_decode_roundtrip_and_oracle(leo, k, r, b, loss):
 MAT_CASES = [(100, 10, 2560, 10, 0), (100, 20, 2560, 20, 0), (128, 128, 65536, 16, 0), (64, 32, 4096, 16, 5),
              (32, 8, 65536, 4, 2), (16, 16, 64, 1, 3), (200, 30, 256, 29, 0), (7, 5, 64 * 9, 3, 1),
              # round 6 (decodes up to L N B = 2^29; output groups of 8; up to 256 inputs)
-             (128, 128, 262144, 8, 120), (128, 128, 65536, 32, 0), (100, 10, 65536, 10, 0), (12, 3, 64 * 1000, 1, 0)]
+             (128, 128, 262144, 8, 120), (128, 128, 65536, 32, 0), (100, 10, 65536, 10, 0), (12, 3, 64 * 1000, 1, 0),
+             (100, 4, 262144, 4, 0)]  # 4-dword lanes (L <= 4 on many strips)
 
 
 @pytest.mark.parametrize("k,r,b,loss,rec_lost", MAT_CASES)

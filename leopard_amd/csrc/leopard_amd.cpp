@@ -975,6 +975,10 @@ LeopardResult encode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
         slice = mall_slice(bytes, slab_pieces);
         slab_bytes = slab_pieces * slice;
     }
+    // narrow columns, several chunks, fewer 16-unit strips than CUs: the chunk
+    // IFFTs in parallel workgroups through a slab of nchunks x m rows
+    const bool split = narrow && encode16_split_wins(Tm, nchunks, bytes / unit_bytes, c.t->cus);
+    if (split) slab_bytes = uint64_t(nchunks) * m * bytes;
     const size_t table_bytes = (mb.bytes() + 255) / 256 * 256;
     LeopardResult r = c.ws->reserve_device(table_bytes + slab_bytes);
     if (r != Leopard_Success) return r;
@@ -983,7 +987,12 @@ LeopardResult encode_device(Call& c, uint64_t bytes, uint64_t off, unsigned K, u
 
     if (narrow) {
         a.nunits = bytes / unit_bytes;
-        HIP_OK(launch_encode16_small(Tm, a, c.s), "encode kernel");
+        if (split) {
+            a.slab_out = a.slab_in = PieceMap{nullptr, c.ws->dbuf + table_bytes, bytes, 0};
+            HIP_OK(launch_encode16_split(Tm, a, c.s), "encode kernels");
+        } else {
+            HIP_OK(launch_encode16_small(Tm, a, c.s), "encode kernel");
+        }
         return Leopard_Success;
     }
     if (!multipass) {

@@ -174,6 +174,11 @@ hipError_t launch_xor_reduce(const XorArgs& a, hipStream_t s);
 // Small GF(2^16) codes on narrow column strips (rs_ff16_small.hip)
 bool encode16_small_supported(unsigned Tm);
 hipError_t launch_encode16_small(unsigned Tm, const EncArgs& a, hipStream_t s);
+// the chunk-parallel form for single calls of few column strips (chunk IFFTs in
+// parallel workgroups into the slab a.slab_out = a.slab_in of nchunks x m rows,
+// then their XOR, the FFT and the outputs)
+bool encode16_split_wins(unsigned Tm, unsigned nchunks, uint64_t nunits, unsigned cus);
+hipError_t launch_encode16_split(unsigned Tm, const EncArgs& a, hipStream_t s);
 // decode, n = 2^Tn with 9 <= Tn <= 11: pass 1 (scale + low IFFT of every tile
 // with received data -> slab a_out), pass 2 (high part + D_lo + low FFT +
 // reveal of every tile holding a lost original, slab a_in = pass 1's)

@@ -22,6 +22,8 @@
 // (Tile::fused_top, as rs_ff8.hip).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "rs_args.h"
 
 namespace lamd {
@@ -270,6 +272,91 @@ __global__ void __launch_bounds__((threads_n<T, R, LW>()), 4) k_enc16n(EncArgs a
 template <int T, int R, int LW>
 __global__ void __launch_bounds__((threads_n<T, R, LW>()), 4) k_enc16n_batch(const EncArgs* __restrict__ objs) {
     enc16n_body<T, R, LW>(objs[blockIdx.y]);
+}
+
+// Chunk-parallel form of enc16n_body for single calls on few column strips
+// (2560-byte pieces: 20 strips of 128 bytes, so the one-kernel form runs 20
+// workgroups, each taking its K / m chunks one after the other).  Pass 1, grid
+// (strips, chunks): chunk c = blockIdx.y's IFFT and fused top layer (one
+// iteration of enc16n_body's chunk loop) into the slab rows c m + slot(r, w);
+// pass 2, grid (strips): the XOR of every chunk's rows (TL::xor_into, by
+// linearity as in enc16n_body), the FFT, the R outputs.  slot(r, w) = r 2^(T-R)
+// + w enumerates the m (register, virtual wave) pairs; both passes use it, so
+// the layout the IFFT ends in need not be named.
+template <int T, int R, int LW>
+LDEV unsigned enc16n_slot(int r, unsigned w) {
+    return unsigned(r) * (1u << (T - R)) + w;
+}
+template <int T, int R, int LW>
+__global__ void __launch_bounds__((threads_n<T, R, LW>()), 4) k_enc16n_part(EncArgs a) {
+    constexpr int G = lg_bits(LW);
+    using TL = Tile<FF16, T, R, 1, LW, 0, G>;
+    constexpr unsigned NT = threads_n<T, R, LW>();
+    constexpr unsigned m = 1u << T;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const unsigned wave = uniform(threadIdx.x >> 6);
+    const unsigned lane = threadIdx.x & (LW - 1);
+    const unsigned w = (wave << G) | ((threadIdx.x & 63u) >> (6 - G));
+    const unsigned c = blockIdx.y;
+    const NarrowCols<LW> cl = narrow_cols<LW>(a.nunits, lane);
+    const PieceSpace ps{0, 0, 0};
+    uint32_t* const set = lds + TL::kXchDwords;
+    typename TL::Reg x;
+    {
+        uint64_t pp[TL::NR];
+        lane_ptrs(pp, a.in, [&](int r) { return min(c * m + TL::piece(0, r, w), a.K - 1); });
+        Tabs16Stage<NT, T> st;
+        st.load(a.sktab, int(m - 1 + c * m), 0, 0);  // chunk c's IFFT skews
+#pragma unroll
+        for (int r = 0; r < TL::NR; ++r) ld_unit(x[r], reinterpret_cast<const uint8_t*>(pp[r]), cl.off);
+        st.store(set);
+#pragma unroll
+        for (int r = 0; r < TL::NR; ++r) {  // the last chunk's zero padding (LeopardFF16.cpp:1446-1448)
+            const bool ok = c * m + TL::piece(0, r, w) < a.K;
+#pragma unroll
+            for (int k = 0; k < TL::U; ++k) x[r][k] = ok ? x[r][k] : 0u;
+        }
+        __syncthreads();
+    }
+    TL::template ifft<true>(x, w, lane, lds, ps, LdsWindow16{set, 0, 0}, AllLive{});
+    TL::fused_top(x, FF16::tab(a.tabs, cload(a.fused + c)));
+    if (!cl.live) return;
+#pragma unroll
+    for (int r = 0; r < TL::NR; ++r) st_unit(a.slab_out.slab_ptr(c * m + enc16n_slot<T, R, LW>(r, w)), cl.off, x[r]);
+}
+template <int T, int R, int LW>
+__global__ void __launch_bounds__((threads_n<T, R, LW>()), 4) k_enc16n_comb(EncArgs a) {
+    constexpr int G = lg_bits(LW);
+    using TL = Tile<FF16, T, R, 1, LW, 0, G>;
+    constexpr unsigned NT = threads_n<T, R, LW>();
+    constexpr unsigned m = 1u << T;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const unsigned wave = uniform(threadIdx.x >> 6);
+    const unsigned lane = threadIdx.x & (LW - 1);
+    const unsigned w = (wave << G) | ((threadIdx.x & 63u) >> (6 - G));
+    const NarrowCols<LW> cl = narrow_cols<LW>(a.nunits, lane);
+    const PieceSpace ps{0, 0, 0};
+    uint32_t* const set = lds + TL::kXchDwords;
+    Tabs16Stage<NT, T> st;
+    st.load(a.sktab, -1, 0, 0);  // FFT skews (base -1)
+    typename TL::Reg acc, x;
+#pragma unroll
+    for (int r = 0; r < TL::NR; ++r) ld_unit(acc[r], a.slab_in.slab_ptr(enc16n_slot<T, R, LW>(r, w)), cl.off);
+    for (unsigned c = 1; c < a.nchunks; ++c) {
+#pragma unroll
+        for (int r = 0; r < TL::NR; ++r) ld_unit(x[r], a.slab_in.slab_ptr(c * m + enc16n_slot<T, R, LW>(r, w)), cl.off);
+        TL::xor_into(acc, x);
+    }
+    st.store(set);
+    __syncthreads();
+    TL::template fft<true>(acc, w, lane, lds, ps, LdsWindow16Static<-1, 0>{{set, 0, 0}}, AllLive{});
+    TL::pin(acc);
+    uint64_t pp[TL::NR];
+    lane_ptrs(pp, a.out, [&](int r) { return min(TL::piece(0, r, w), a.R - 1); });
+    if (!cl.live) return;
+#pragma unroll
+    for (int r = 0; r < TL::NR; ++r)
+        if (TL::piece(0, r, w) < a.R) st_unit(reinterpret_cast<uint8_t*>(pp[r]), cl.off, acc[r]);
 }
 
 template <int T, int R, int LW>
@@ -952,6 +1039,44 @@ hipError_t launch_encode16_small(unsigned Tm, const EncArgs& a, hipStream_t s) {
     switch (Tm) {
         case 7: return wide ? launch_enc16n<7, 3, 32>(a, s) : launch_enc16n<7, 3, 16>(a, s);
         case 8: return launch_enc16n<8, 3, 16>(a, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+// The chunk-parallel form (k_enc16n_part + k_enc16n_comb, 16-unit strips) for
+// single calls with several chunks on fewer 16-unit strips than CUs; the slab
+// (a.slab_out = a.slab_in) holds nchunks x m rows of the piece width.
+bool encode16_split_wins(unsigned Tm, unsigned nchunks, uint64_t nunits, unsigned cus) {
+    bool win = encode16_small_supported(Tm) && nchunks >= 2 && (nunits + 15) / 16 < cus;
+#if LAMD_EXPERIMENT_ENV
+    static const int force = [] {
+        const char* e = std::getenv("LEO_AMD_ENC16_SPLIT");
+        return e ? (e[0] == '1' ? 1 : 0) : -1;
+    }();
+    if (force >= 0) win = encode16_small_supported(Tm) && nchunks >= 2 && force == 1;
+#endif
+    return win;
+}
+hipError_t launch_encode16_split(unsigned Tm, const EncArgs& a, hipStream_t s) {
+    auto go = [&](auto part, auto comb, unsigned threads, size_t lds) {
+        for (const void* fn : {reinterpret_cast<const void*>(part), reinterpret_cast<const void*>(comb)}) {
+            const hipError_t attr = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+            if (attr != hipSuccess) return attr;
+        }
+        void* params[] = {const_cast<EncArgs*>(&a)};
+        const unsigned strips = unsigned((a.nunits + 15) / 16);
+        hipError_t e = hipLaunchKernel(reinterpret_cast<const void*>(part), dim3(strips, a.nchunks), dim3(threads), params,
+                                       lds, s);
+        if (e != hipSuccess) return e;
+        return hipLaunchKernel(reinterpret_cast<const void*>(comb), dim3(strips), dim3(threads), params, lds, s);
+    };
+    using TL7 = Tile<FF16, 7, 3, 1, 16, 0, lg_bits(16)>;
+    using TL8 = Tile<FF16, 8, 3, 1, 16, 0, lg_bits(16)>;
+    switch (Tm) {
+        case 7: return go(&k_enc16n_part<7, 3, 16>, &k_enc16n_comb<7, 3, 16>, threads_n<7, 3, 16>(),
+                          (TL7::kXchDwords + tab16_set_dwords(7)) * 4);
+        case 8: return go(&k_enc16n_part<8, 3, 16>, &k_enc16n_comb<8, 3, 16>, threads_n<8, 3, 16>(),
+                          (TL8::kXchDwords + tab16_set_dwords(8)) * 4);
         default: return hipErrorInvalidValue;
     }
 }

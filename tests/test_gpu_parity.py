@@ -1035,3 +1035,46 @@ def test_concurrent_host_threads_are_reentrant(leo):
             th.join(timeout=90)
         assert not any(th.is_alive() for th in threads), "a worker thread hung"
     assert not errors, errors
+
+
+_FORCED_ENC16 = r"""
+import sys
+sys.path.insert(0, {repo!r}); sys.path.insert(0, {tests!r})
+import numpy as np
+import leopard_amd as leo, test_gpu_parity as t, oracle_lib as ol
+assert leo.leo_init() == 0
+for k, r, b in {cases!r}:
+    data = np.random.default_rng(k + r + b).integers(0, 256, (k, b), dtype=np.uint8)
+    assert np.array_equal(t.gpu_encode(leo, data, r), ol.oracle().encode(data, r)), (k, r, b)
+print("forced ok")
+"""
+ENC16_SPLIT_CASES = [(1000, 200, 2560), (300, 100, 64 * 37), (129, 127, 64), (700, 256, 128), (513, 200, 64 * 40)]
+
+
+@pytest.mark.parametrize("k,r,b", ENC16_SPLIT_CASES)
+def test_ff16_chunk_parallel_encode_matches_oracle(leo, k, r, b):
+    """Single GF(2^16) encodes with m <= 256, several chunks and fewer 16-unit
+    column strips than CUs (rs_ff16_small.hip k_enc16n_part + k_enc16n_comb):
+    a zero-padded last chunk (K not a multiple of m), a partial last strip
+    (64 x 37-byte pieces), m = 128 and m = 256."""
+    rng = np.random.default_rng(k * 3 + r + b)
+    data = rng.integers(0, 256, (k, b), dtype=np.uint8)
+    assert np.array_equal(gpu_encode(leo, data, r), ol.oracle().encode(data, r))
+
+
+@pytest.mark.parametrize("split", ["0", "1"])
+def test_ff16_encode_forced_forms_match_oracle(split):
+    """Both narrow GF(2^16) encode forms on both sides of the split rule: the
+    experiment build with LEO_AMD_ENC16_SPLIT=0 (one kernel, also on few strips)
+    or =1 (chunk-parallel, also on many strips), in a child process."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    repo = os.path.dirname(here)
+    lib = os.path.join(repo, "leopard_amd", "lib", "exp", "libleopard_amd.so")
+    assert os.path.exists(lib), "make -C leopard_amd builds lib/exp"
+    cases = ENC16_SPLIT_CASES + [(1000, 200, 65536), (300, 100, 8192)]
+    env = dict(os.environ, LEOPARD_AMD_LIB=lib, LEO_AMD_ENC16_SPLIT=split)
+    p = subprocess.run([sys.executable, "-c", _FORCED_ENC16.format(repo=repo, tests=here, cases=cases)], env=env,
+                       capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0 and "forced ok" in p.stdout, (p.stdout[-2000:], p.stderr[-3000:])

@@ -987,7 +987,10 @@ hipError_t launch16n(Kern* fn, dim3 grid, unsigned threads, size_t lds_bytes, co
     return hipLaunchKernel(reinterpret_cast<const void*>(fn), grid, dim3(threads), params, lds_bytes, s);
 }
 
-constexpr int kDecR = 3, kDecLW = 16, kDecNZ = LAMD_DEC16N_NZ;
+#ifndef LAMD_DEC16N_R  // registers bits of the narrow decoder tiles (experiment builds: 2)
+#define LAMD_DEC16N_R 3
+#endif
+constexpr int kDecR = LAMD_DEC16N_R, kDecLW = 16, kDecNZ = LAMD_DEC16N_NZ;
 using DecTL = Tile<FF16, 8, kDecR, 1, kDecLW, 0, lg_bits(kDecLW)>;
 constexpr size_t kDecLds = (DecTL::kXchDwords + tab16_set_dwords(8)) * 4;
 constexpr size_t kDecFinLds = (DecTL::kXchDwords + kDecNZ * tab16_set_dwords(8)) * 4;

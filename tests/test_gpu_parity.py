@@ -1078,3 +1078,33 @@ def test_ff16_encode_forced_forms_match_oracle(split):
     p = subprocess.run([sys.executable, "-c", _FORCED_ENC16.format(repo=repo, tests=here, cases=cases)], env=env,
                        capture_output=True, text=True, timeout=110)
     assert p.returncode == 0 and "forced ok" in p.stdout, (p.stdout[-2000:], p.stderr[-3000:])
+
+
+_FORCED_MAT = r"""
+import sys
+sys.path.insert(0, {repo!r}); sys.path.insert(0, {tests!r})
+import leopard_amd as leo, test_gpu_parity as t
+assert leo.leo_init() == 0
+for c in {cases!r}:
+    t.test_matrix_path_matches_oracle(leo, *c)
+print("forced ok")
+"""
+
+
+@pytest.mark.parametrize("c,lb", [("1", "1"), ("1", "8"), ("2", "2"), ("2", "8"), ("4", "1"), ("4", "4")])
+def test_matrix_kernel_forced_shapes_match_oracle(c, lb):
+    """Every lane width C and output group LB of k_ff8_mat (experiment build,
+    LEO_AMD_MAT_C / LEO_AMD_MAT_LB), on inputs per wave KI = 1 .. 16 and output
+    counts that leave a partial group, in a child process."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    repo = os.path.dirname(here)
+    lib = os.path.join(repo, "leopard_amd", "lib", "exp", "libleopard_amd.so")
+    assert os.path.exists(lib), "make -C leopard_amd builds lib/exp"
+    cases = [(100, 10, 2560, 10, 0), (128, 128, 65536, 16, 0), (12, 3, 64 * 1000, 1, 0), (16, 16, 64, 1, 3),
+             (32, 8, 65536, 4, 2), (200, 30, 256, 29, 0)]
+    env = dict(os.environ, LEOPARD_AMD_LIB=lib, LEO_AMD_MAT_C=c, LEO_AMD_MAT_LB=lb)
+    p = subprocess.run([sys.executable, "-c", _FORCED_MAT.format(repo=repo, tests=here, cases=cases)], env=env,
+                       capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0 and "forced ok" in p.stdout, (p.stdout[-2000:], p.stderr[-3000:])
